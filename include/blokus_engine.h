@@ -1,0 +1,166 @@
+/*
+ * blokus_engine.h — C-ABI of the MI355X-native Blokus engine (libblokus_hip.so).
+ *
+ * This is the drop-in boundary for the reference's hot path. The reference
+ * reaches its rules engine (the un-vendored `colosseumrl.envs.blokus`, setup.py:11) through
+ * `ColosseumBlokusGameWrapper` (blokus_rl/colossumrl/blokus_wrapper.py:21) and its search through
+ * `MCTS` (blokus_rl/alphazero/mcts.py:7). Every entry point below names the reference interface
+ * it replaces. The Python mirror of those classes (blokus_rl_amd/) binds this header via ctypes;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain C types only. Device buffers are raw device pointers (e.g. torch `data_ptr()`),
+ *     caller-owned, and every launch takes a `stream` (a hipStream_t passed as void*; NULL =
+ *     the null stream). No call synchronises unless its comment says so.
+ *   - Return 0 on success, a negative BK_E* code on failure; bk_last_error() returns text.
+ *   - One context per stream; a context is not thread-safe.
+ *   - States are values: no call mutates an input state (blokus_wrapper.py:89-106 semantics).
+ */
+#ifndef BLOKUS_ENGINE_H
+#define BLOKUS_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- error codes */
+#define BK_OK 0
+#define BK_EINVAL -1    /* bad argument (null pointer, size, preset)            */
+#define BK_EHIP -2      /* a HIP runtime call failed                             */
+#define BK_EILLEGAL -3  /* an action is not legal in its state (next_state)     */
+#define BK_ECAPACITY -4 /* an MCTS pool/table ran out of room                    */
+#define BK_ENOMEM -5
+
+/* ---------------------------------------------------------------- packed state
+ * One game state = 384 bytes (6 x 64 B), 64-B aligned in arrays. Byte layout:
+ *   [  0,320) uint32 occ[4][20]   occupancy bitboard per colour; row r, bit c = cell (r,c).
+ *                                 Colours 0..P-1 = reference colours 1..P
+ *                                 (blokus_wrapper.py:259 colour map).
+ *   [320,336) uint32 pieces[4]    bit i set = piece i still unused by that colour.
+ *   [336,344) uint64 hash         64-bit hash of the board contents only (occ), the analogue
+ *                                 of hash(board_contents.tobytes()) (blokus_wrapper.py:208-218).
+ *   [344,348) int32  to_move      player to move (reference `current_player`).
+ *   [348,352) int32  ply          placements made so far.
+ *   [352,356) uint32 flags        bit0 = game over (nobody can move);
+ *                                 bits 4..7 = player known to have no legal move (cache).
+ *   [356,384) reserved, zero.
+ */
+#define BK_STATE_BYTES 384
+#define BK_MAX_N 20
+#define BK_MAX_P 4
+
+typedef struct bk_ctx bk_ctx;
+typedef struct bk_mcts bk_mcts;
+
+const char* bk_last_error(void);
+int bk_version(void);
+int bk_state_bytes(void);
+
+/* ---------------------------------------------------------------- context / presets
+ * board_size N (5..20), num_players P (2 or 4), max_piece_cells (1..5).
+ * Presets used by the reference: (20,4,5) -> 30433 actions (docs/README.md:128);
+ * (7,2,4) -> 919 actions (docs/README.md:51); (7,2,5) -> 2522 (the 7x7 recordings).
+ * Replaces: BlokusEnvironment() + _set_all_possible_moves (blokus_wrapper.py:42, :281-324). */
+int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int device, bk_ctx** out);
+int bk_ctx_destroy(bk_ctx* ctx);
+/* get_action_size (blokus_wrapper.py:59-64). */
+int bk_action_size(const bk_ctx* ctx);
+/* Number of u64 words of one legal-move bitmask = ceil(A/64). */
+int bk_mask_words(const bk_ctx* ctx);
+/* Host copy of the action table: out[4*id + {0,1,2,3}] = {piece, orientation, row, col} of
+ * the placement's bounding-box origin. Canonical id order = (piece, orientation, row, col).
+ * Replaces the action-string <-> id dicts (blokus_wrapper.py:37-38, :313-318). */
+int bk_action_table(const bk_ctx* ctx, int32_t* out);
+/* Host copy of the placement cells: out[5*id + k] = row*N + col of cell k, -1 padded. */
+int bk_action_cells(const bk_ctx* ctx, int16_t* out);
+/* Piece count in this preset (21 at max_piece_cells 5, 9 at 4). */
+int bk_num_pieces(const bk_ctx* ctx);
+
+/* ---------------------------------------------------------------- batched env (device)
+ * get_init_board (blokus_wrapper.py:80-87): B fresh states, player 0 to move. */
+int bk_init_states(bk_ctx* ctx, void* states, int B, void* stream);
+
+/* get_valid_moves (blokus_wrapper.py:108-132) for B states. players[b] = player whose moves
+ * are listed, or -1 (or players == NULL) for the state's to_move (the wrapper's -1 convention,
+ * :119-121). mask_words: [B][bk_mask_words] u64, bit id set = legal. counts: [B] int32 (may be
+ * NULL). Legality = cells empty, no own-colour edge contact, >=1 own-colour corner contact
+ * (own start corner on the colour's first placement), piece unused. */
+int bk_legal_mask(bk_ctx* ctx, const void* states, const int32_t* players, int B,
+                  uint64_t* mask_words, int32_t* counts, void* stream);
+
+/* get_next_state (blokus_wrapper.py:89-106) for B states: place actions[b] for the state's
+ * to_move, retire the piece, then pass the turn to the next player in cyclic order who has a
+ * legal move (skip rule); nobody -> game over. states_out may alias nothing in states_in.
+ * next_players: [B] int32 (may be NULL). status: [B] int32 (may be NULL): 0 ok, 1 illegal
+ * action (state copied unchanged). actions[b] < 0 -> state copied unchanged (status 0). */
+int bk_next_state(bk_ctx* ctx, const void* states_in, const int32_t* actions, int B,
+                  void* states_out, int32_t* next_players, int32_t* status, void* stream);
+
+/* get_game_ended (blokus_wrapper.py:164-186): ended[b] = 1 when nobody can move; then
+ * scores[b][P] = -1 for losers, 3 for a sole winner, 1 for each tied winner (winner = most
+ * squares placed); 0-filled when not ended. */
+int bk_game_ended(bk_ctx* ctx, const void* states, int B, int32_t* ended, double* scores,
+                  void* stream);
+
+/* Board.canonical_board via get_observation (blokus_wrapper.py:134-146): obs[B][2P][N][N] f32;
+ * planes 0..P-1 = colour occupancy (absolute orientation), plane P+to_move = all ones. */
+int bk_observe(bk_ctx* ctx, const void* states, int B, float* obs, void* stream);
+
+/* Squares placed per colour: out[B][P] int32 (scoring input of get_winners). */
+int bk_square_counts(bk_ctx* ctx, const void* states, int B, int32_t* out, void* stream);
+
+/* Compact legal ids: ids[b][0..K) ascending (the np.where(mask) order of mcts.py:64),
+ * counts[b] = K; rows are `cap` ids wide (K > cap -> BK_ECAPACITY flagged in counts as -K). */
+int bk_legal_ids(bk_ctx* ctx, const void* states, const int32_t* players, int B, int32_t* ids,
+                 int cap, int32_t* counts, void* stream);
+
+/* ---------------------------------------------------------------- batched MCTS (device)
+ * T independent search trees (one per game), one simulation in flight per tree, which keeps
+ * each tree's sequence of simulations identical to MCTS.simulate (mcts.py:13-71). A tree is a
+ * transposition table keyed by the board hash (mcts.py:37-39) with SoA child statistics
+ * {id, N, Q (f64), P (f32)}; it persists across moves of one game (trainer.py:95).
+ *   node_cap  : nodes per tree (hash table sized to 2x that, power of two)
+ *   child_cap : children in the shared pool across all trees */
+int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_mcts** out);
+int bk_mcts_destroy(bk_mcts* m);
+/* Clear the trees whose flag is non-zero (reset_flags: [T] int32 device, NULL = all):
+ * MCTSPlayer.reset / a new MCTS(game, nn) per episode (mcts_player.py:24-25, trainer.py:95). */
+int bk_mcts_reset(bk_mcts* m, const int32_t* reset_flags, void* stream);
+
+/* One selection pass (the descent half of simulate, mcts.py:37-50 and :58-65): for every tree
+ * with active[t] != 0 descend from roots[t] by argmax(Q + cpuct*P*sqrt(sum N + 1e-6)/(1+N))
+ * (first max; cpuct only at the root, as mcts.py:50 passes none further) until a board not in
+ * the table or a terminal board. Outputs per tree:
+ *   leaf_status[t]: 0 inactive, 1 needs NN evaluation, 2 terminal (value = one-hot scores)
+ *   obs[t]: the leaf observation [2P][N][N] f32 (written for status 1) — the NN input batch
+ *   leaf_mask: [T][mask_words] legal bits of the leaf (status 1), for the masked softmax. */
+int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double cpuct,
+                   int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream);
+
+/* Expansion + backup (mcts.py:50-56 and :63-70): for status-1 leaves create the node with
+ * P = exp(log_softmax(logp[t][legal ids])) (neural_network.py:159-173) and back up
+ * values[t][P]; for status-2 leaves back up the terminal scores. logp: [T][A] f32 (the net's
+ * log-softmax output, rows of inactive/terminal trees ignored); values: [T][P] f32. */
+int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, void* stream);
+
+/* get_distribution (mcts.py:73-99) at the root of every active tree: ids[t][0..K) and
+ * pi[t][0..K) (f64) in child order, K in counts[t]; temperature 0 -> one-hot argmax N
+ * (first max); all-zero N -> uniform. Rows are `cap` wide. Root must be expanded. */
+int bk_mcts_root_policy(bk_mcts* m, const void* roots, const int32_t* active, double temperature,
+                        int32_t* ids, double* pi, int cap, int32_t* counts, void* stream);
+
+/* Root child statistics (for tests / players): n[t][cap] u32, q[t][cap] f64, p[t][cap] f32. */
+int bk_mcts_root_stats(bk_mcts* m, const void* roots, const int32_t* active, int32_t* ids,
+                       uint32_t* n, double* q, float* p, int cap, int32_t* counts, void* stream);
+
+/* Engine counters (host copy, synchronises the stream): out[0] nodes used (all trees),
+ * out[1] children used, out[2] selection levels descended (cumulative), out[3] leaves
+ * expanded, out[4] terminal leaves, out[5] error flags (bit0 child pool full, bit1 table full). */
+int bk_mcts_counters(bk_mcts* m, int64_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLOKUS_ENGINE_H */
