@@ -1,0 +1,207 @@
+"""Benchmark of the Blokus hot path on MI355X (contract: one JSON line from rank 0).
+
+Workloads (BASELINE.json configs):
+  legal    — config 2: legal-move bitmasks of 4096 random 20x20 boards per step (one
+             k_legal_mask launch over the batch), metric = boards/s.
+  selfplay — config 3/4: AlphaZero self-play, 256 concurrent 4-player 20x20 games per GPU,
+             100 MCTS simulations per move, ResNet leaf evaluation; metric = MCTS sims/s.
+
+Multi-GPU: one process per GPU (torchrun); every rank runs its own independent shard (boards /
+games seeded by rank), no data-path collective; value = units of all ranks / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
+
+# Algorithmic bytes of one board in k_legal_mask: the packed state read (384 B) + the
+# 30433-bit mask written (476 u64 = 3808 B) + its count (4 B). DESIGN.md §4.
+LEGAL_BYTES_PER_BOARD = 384 + 3808 + 4
+
+
+def _dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def _barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def _max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
+    if one exists for this kernel; FETCH_SIZE doubled per the gfx950 correction
+    (MI355X_MICROARCH.md §HBM). None when absent."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for fp in reversed(files):
+        try:
+            with open(fp, encoding="utf-8") as f:
+                d = json.load(f)
+            k = d.get("kernels", {}).get(kernel_prefix)
+            if k and k.get("units_per_launch") == units_per_launch:
+                return float(k["hbm_bytes_per_launch"])
+        except Exception:
+            continue
+    return None
+
+
+# ----------------------------------------------------------------------------- legal
+def bench_legal(args, world, rank):
+    from blokus_rl_amd.boards import random_boards
+    from blokus_rl_amd.engine import Engine
+
+    B = args.boards
+    eng = Engine(20, 4, 5)
+    states = random_boards(eng, B, seed0=rank * B)
+    masks = torch.empty((B, eng.W), dtype=torch.int64, device=eng.device)
+    counts = torch.empty(B, dtype=torch.int32, device=eng.device)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        eng.legal_mask_into(states, masks, counts)
+
+    graph = None
+    if args.graph:
+        # capture `graph_steps` back-to-back passes; replay = graph_steps steps
+        s = torch.cuda.Stream()
+        s.wait_stream(stream)
+        with torch.cuda.stream(s):
+            step()
+        stream.wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(args.graph_steps):
+                step()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    if graph is not None:
+        reps = max(1, args.steps // args.graph_steps)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            graph.replay()
+        e1.record(stream)
+        steps_done = reps * args.graph_steps
+    else:
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            step()
+            ev[i][1].record(stream)
+        steps_done = args.steps
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed = _max_over_ranks(t1 - t0, world)
+    if graph is not None:
+        kernel_ms = e0.elapsed_time(e1) / steps_done
+    else:
+        kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    boards_total = B * steps_done * world
+    value = boards_total / elapsed
+    achieved = LEGAL_BYTES_PER_BOARD * B / (kernel_ms * 1e-3)
+    traffic = _pmc_traffic("k_legal_mask", B)
+    out = {
+        "metric": "legal-move boards/sec (20x20, 4 players, 30433-id bitmask)",
+        "value": value,
+        "unit": "boards/s",
+        "n_gpus": world,
+        "steps": steps_done,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / steps_done * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32/u64 bitboards",
+        "data": "synthetic: default_rng(b) random self-play boards, t~U{0..60} plies",
+        "config": {"workload": "config 2: 20x20 legal-move enumeration, batch 4096 boards per GPU",
+                   "global_batch": B * world, "parallelism": f"dp{world} (independent shards)",
+                   "graph": bool(args.graph)},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "kernel": "k_legal_mask", "kernel_ms": kernel_ms,
+                     "bytes_per_unit": LEGAL_BYTES_PER_BOARD, "units_per_launch": B},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_legal(states, args.cpu_seconds)
+    return out
+
+
+def cpu_baseline_legal(states: torch.Tensor, seconds: float):
+    """The oracle (C restatement of the reference rules, 1 core) on a bounded sample of the
+    same boards: repeat over the first 256 boards until `seconds` of CPU work."""
+    from oracle.oracle import Oracle
+
+    o = Oracle(20, 4, 5)
+    sample = states[:256].cpu().numpy()
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.legal_mask_batch(sample)
+        n += sample.shape[0]
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "boards/s", "cores": 1, "kind": "port",
+            "sample": f"{n} board evaluations (first 256 benchmark boards, repeated) in {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", choices=["legal", "selfplay"], default="legal")
+    ap.add_argument("--boards", type=int, default=4096)
+    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--graph-steps", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world, rank, _ = _dist_init()
+    if args.workload == "legal":
+        out = bench_legal(args, world, rank)
+    else:
+        from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay
+        out = bench_selfplay(args, world, rank)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,31 @@
+// ctx.h — host-side context of the engine library (one board preset on one device).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "common.h"
+#include "tables.h"
+
+struct bk_ctx {
+  bk::Preset pre;
+  bk::DevPreset dp;
+  int device = 0;
+  uint64_t* d_items = nullptr;
+  uint32_t* d_act = nullptr;
+};
+
+namespace bk {
+void set_error(const std::string& msg);
+int hip_check(hipError_t e, const char* what);
+// Launch-error check after a kernel launch.
+int launch_check(const char* what);
+}  // namespace bk
+
+#define BK_REQUIRE(cond, msg)            \
+  do {                                   \
+    if (!(cond)) {                       \
+      bk::set_error(msg);                \
+      return BK_EINVAL;                  \
+    }                                    \
+  } while (0)

@@ -1,0 +1,286 @@
+// env.hip — batched Blokus rules engine on gfx950 + the env half of the C-ABI
+// (include/blokus_engine.h). One 64-lane wave per board; see common.h.
+#include <cstring>
+#include <string>
+
+#include "../../include/blokus_engine.h"
+#include "ctx.h"
+
+namespace bk {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return BK_OK;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return BK_EHIP;
+}
+int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
+
+namespace {
+
+__global__ void k_init_states(DevPreset dp, uint32_t* states, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * kStateWords) return;
+  const int w = i % kStateWords;
+  uint32_t v = 0;
+  if (w >= kWPieces && w < kWPieces + kMaxP) v = (w - kWPieces) < dp.P ? dp.full_pieces : 0u;
+  if (w == kWHash) v = 0x7F4A7C15u;      // hash of the empty board = the seed
+  if (w == kWHash + 1) v = 0x9E3779B9u;
+  states[i] = v;
+}
+
+// Legal-move bitmask of B boards. Grid = B blocks of one wave.
+__global__ __launch_bounds__(64) void k_legal_mask(DevPreset dp, const uint32_t* __restrict__ states,
+                                                   const int32_t* __restrict__ players, int B,
+                                                   uint64_t* __restrict__ masks, int32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* s = lds;                                   // 96 words
+  uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);  // 20 u64
+  uint32_t* m32 = lds + kStateWords + 2 * kMaxN;       // W32pad words
+  const int b = blockIdx.x;
+  const int l = lane_id();
+  load_state(s, states + (size_t)b * kStateWords);
+  __syncthreads();
+  int q = players ? players[b] : -1;
+  if (q < 0) q = (int)s[kWToMove];
+  build_mask(dp, s, q, fa, m32);
+  int cnt = 0;
+  uint64_t* out = masks + (size_t)b * dp.W64;
+  for (int j = l; j < dp.W64; j += kWave) {
+    const uint64_t w = (uint64_t)m32[2 * j] | ((uint64_t)m32[2 * j + 1] << 32);
+    cnt += __popcll(w);
+    out[j] = w;
+  }
+  cnt = wave_sum(cnt);
+  if (counts && l == 0) counts[b] = cnt;
+}
+
+__global__ __launch_bounds__(64) void k_legal_ids(DevPreset dp, const uint32_t* __restrict__ states,
+                                                  const int32_t* __restrict__ players, int B, int32_t* ids,
+                                                  int cap, int32_t* counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* s = lds;
+  uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
+  uint32_t* m32 = lds + kStateWords + 2 * kMaxN;
+  const int b = blockIdx.x;
+  load_state(s, states + (size_t)b * kStateWords);
+  __syncthreads();
+  int q = players ? players[b] : -1;
+  if (q < 0) q = (int)s[kWToMove];
+  build_mask(dp, s, q, fa, m32);
+  const int K = compact_ids(dp, m32, ids + (size_t)b * cap, cap);
+  if (lane_id() == 0) counts[b] = K <= cap ? K : -K;
+}
+
+__global__ __launch_bounds__(64) void k_next_state(DevPreset dp, const uint32_t* __restrict__ in,
+                                                   const int32_t* __restrict__ actions, int B, uint32_t* out,
+                                                   int32_t* next_players, int32_t* status) {
+  __shared__ __attribute__((aligned(16))) uint32_t s[kStateWords];
+  __shared__ uint64_t fa[kMaxN];
+  const int b = blockIdx.x;
+  load_state(s, in + (size_t)b * kStateWords);
+  __syncthreads();
+  const int a = actions[b];
+  int st = 0;
+  if (a >= 0) st = apply_action(dp, s, a, fa);
+  store_state(out + (size_t)b * kStateWords, s);
+  if (lane_id() == 0) {
+    if (next_players) next_players[b] = (int)s[kWToMove];
+    if (status) status[b] = st;
+  }
+}
+
+__global__ void k_game_ended(DevPreset dp, const uint32_t* __restrict__ states, int B, int32_t* ended,
+                             double* scores) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint32_t* s = states + (size_t)b * kStateWords;
+  const bool over = s[kWFlags] & kFlagOver;
+  if (ended) ended[b] = over ? 1 : 0;
+  if (!scores) return;
+  double sc[kMaxP];
+  if (over) {
+    terminal_scores(dp, s, sc);
+  } else {
+    for (int k = 0; k < kMaxP; ++k) sc[k] = 0.0;
+  }
+  for (int k = 0; k < dp.P; ++k) scores[(size_t)b * dp.P + k] = sc[k];
+}
+
+__global__ void k_square_counts(DevPreset dp, const uint32_t* __restrict__ states, int B, int32_t* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint32_t* s = states + (size_t)b * kStateWords;
+  for (int k = 0; k < dp.P; ++k) out[(size_t)b * dp.P + k] = squares_of(dp, s, k);
+}
+
+// Observation planes [2P][N][N] f32 (Board.canonical_board, blokus_wrapper.py:146): one block
+// of 256 threads per board, each thread a run of cells.
+__global__ __launch_bounds__(256) void k_observe(DevPreset dp, const uint32_t* __restrict__ states, int B,
+                                                 float* __restrict__ obs) {
+  const int b = blockIdx.x;
+  const uint32_t* s = states + (size_t)b * kStateWords;
+  const int NN = dp.N * dp.N;
+  const int total = 2 * dp.P * NN;
+  const int tm = (int)s[kWToMove];
+  float* o = obs + (size_t)b * total;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int plane = i / NN, cell = i - plane * NN;
+    float v;
+    if (plane < dp.P) {
+      const int r = cell / dp.N, c = cell - r * dp.N;
+      v = (float)((s[plane * kMaxN + r] >> c) & 1u);
+    } else {
+      v = (plane - dp.P) == tm ? 1.0f : 0.0f;
+    }
+    o[i] = v;
+  }
+}
+
+}  // namespace
+}  // namespace bk
+
+using namespace bk;
+
+static size_t mask_lds_bytes(const DevPreset& dp) {
+  return sizeof(uint32_t) * (size_t)(kStateWords + 2 * kMaxN + dp.W32pad);
+}
+
+extern "C" {
+
+const char* bk_last_error(void) { return g_last_error.c_str(); }
+int bk_version(void) { return 1; }
+int bk_state_bytes(void) { return BK_STATE_BYTES; }
+
+int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int device, bk_ctx** out) {
+  BK_REQUIRE(out, "out is null");
+  *out = nullptr;
+  bk_ctx* c = new bk_ctx();
+  if (!build_preset(board_size, num_players, max_piece_cells, &c->pre)) {
+    delete c;
+    set_error("unsupported preset");
+    return BK_EINVAL;
+  }
+  c->device = device;
+  const Preset& p = c->pre;
+  DevPreset& d = c->dp;
+  d.N = p.N; d.P = p.P; d.A = p.A; d.W64 = p.mask_words; d.W32 = p.mask_words32;
+  d.W32pad = 2 * p.mask_words;
+  d.num_items = p.num_items; d.num_pieces = p.num_pieces;
+  d.full_pieces = p.full_pieces;
+  d.full_row = (1u << p.N) - 1u;
+  for (int k = 0; k < kMaxP; ++k) { d.corner_r[k] = (int8_t)p.corner_r[k]; d.corner_c[k] = (int8_t)p.corner_c[k]; }
+  for (int i = 0; i <= kNumPieces; ++i) d.piece_item_off[i] = (int16_t)p.piece_item_off[i];
+  if (device < 0) {  // host-only context: tables, no device memory (CPU tests, tooling)
+    *out = c;
+    return BK_OK;
+  }
+  int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+  if (rc) { delete c; return rc; }
+  rc = hip_check(hipMalloc(&c->d_items, sizeof(uint64_t) * p.items.size()), "hipMalloc items");
+  if (!rc) rc = hip_check(hipMalloc(&c->d_act, sizeof(uint32_t) * p.act.size()), "hipMalloc act");
+  if (!rc) rc = hip_check(hipMemcpy(c->d_items, p.items.data(), sizeof(uint64_t) * p.items.size(),
+                                    hipMemcpyHostToDevice), "copy items");
+  if (!rc) rc = hip_check(hipMemcpy(c->d_act, p.act.data(), sizeof(uint32_t) * p.act.size(),
+                                    hipMemcpyHostToDevice), "copy act");
+  if (rc) { bk_ctx_destroy(c); return rc; }
+  d.items = c->d_items;
+  d.act = c->d_act;
+  *out = c;
+  return BK_OK;
+}
+
+int bk_ctx_destroy(bk_ctx* c) {
+  if (!c) return BK_OK;
+  if (c->d_items) (void)hipFree(c->d_items);
+  if (c->d_act) (void)hipFree(c->d_act);
+  delete c;
+  return BK_OK;
+}
+
+int bk_action_size(const bk_ctx* c) { return c ? c->pre.A : BK_EINVAL; }
+int bk_mask_words(const bk_ctx* c) { return c ? c->pre.mask_words : BK_EINVAL; }
+int bk_num_pieces(const bk_ctx* c) { return c ? c->pre.num_pieces : BK_EINVAL; }
+
+int bk_action_table(const bk_ctx* c, int32_t* out) {
+  BK_REQUIRE(c && out, "null argument");
+  std::memcpy(out, c->pre.act_table.data(), sizeof(int32_t) * c->pre.act_table.size());
+  return BK_OK;
+}
+
+int bk_action_cells(const bk_ctx* c, int16_t* out) {
+  BK_REQUIRE(c && out, "null argument");
+  std::memcpy(out, c->pre.act_cells.data(), sizeof(int16_t) * c->pre.act_cells.size());
+  return BK_OK;
+}
+
+int bk_init_states(bk_ctx* c, void* states, int B, void* stream) {
+  BK_REQUIRE(c && states && B >= 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  if (B == 0) return BK_OK;
+  const int n = B * kStateWords;
+  hipLaunchKernelGGL(k_init_states, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, c->dp,
+                     (uint32_t*)states, B);
+  return launch_check("k_init_states");
+}
+
+int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, uint64_t* mask_words,
+                  int32_t* counts, void* stream) {
+  BK_REQUIRE(c && states && mask_words && B >= 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  if (B == 0) return BK_OK;
+  hipLaunchKernelGGL(k_legal_mask, dim3(B), dim3(kWave), mask_lds_bytes(c->dp), (hipStream_t)stream, c->dp,
+                     (const uint32_t*)states, players, B, mask_words, counts);
+  return launch_check("k_legal_mask");
+}
+
+int bk_legal_ids(bk_ctx* c, const void* states, const int32_t* players, int B, int32_t* ids, int cap,
+                 int32_t* counts, void* stream) {
+  BK_REQUIRE(c && states && ids && counts && B >= 0 && cap > 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  if (B == 0) return BK_OK;
+  hipLaunchKernelGGL(k_legal_ids, dim3(B), dim3(kWave), mask_lds_bytes(c->dp), (hipStream_t)stream, c->dp,
+                     (const uint32_t*)states, players, B, ids, cap, counts);
+  return launch_check("k_legal_ids");
+}
+
+int bk_next_state(bk_ctx* c, const void* states_in, const int32_t* actions, int B, void* states_out,
+                  int32_t* next_players, int32_t* status, void* stream) {
+  BK_REQUIRE(c && states_in && actions && states_out && B >= 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  BK_REQUIRE(states_in != states_out, "states_out must not alias states_in");
+  if (B == 0) return BK_OK;
+  hipLaunchKernelGGL(k_next_state, dim3(B), dim3(kWave), 0, (hipStream_t)stream, c->dp,
+                     (const uint32_t*)states_in, actions, B, (uint32_t*)states_out, next_players, status);
+  return launch_check("k_next_state");
+}
+
+int bk_game_ended(bk_ctx* c, const void* states, int B, int32_t* ended, double* scores, void* stream) {
+  BK_REQUIRE(c && states && B >= 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  if (B == 0) return BK_OK;
+  hipLaunchKernelGGL(k_game_ended, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->dp,
+                     (const uint32_t*)states, B, ended, scores);
+  return launch_check("k_game_ended");
+}
+
+int bk_square_counts(bk_ctx* c, const void* states, int B, int32_t* out, void* stream) {
+  BK_REQUIRE(c && states && out && B >= 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  if (B == 0) return BK_OK;
+  hipLaunchKernelGGL(k_square_counts, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->dp,
+                     (const uint32_t*)states, B, out);
+  return launch_check("k_square_counts");
+}
+
+int bk_observe(bk_ctx* c, const void* states, int B, float* obs, void* stream) {
+  BK_REQUIRE(c && states && obs && B >= 0, "bad argument");
+  BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
+  if (B == 0) return BK_OK;
+  hipLaunchKernelGGL(k_observe, dim3(B), dim3(256), 0, (hipStream_t)stream, c->dp, (const uint32_t*)states, B,
+                     obs);
+  return launch_check("k_observe");
+}
+
+}  // extern "C"

@@ -1,0 +1,510 @@
+// mcts.hip — batched AlphaZero MCTS on gfx950 (the search half of the C-ABI).
+//
+// T independent trees, one per game, one simulation in flight per tree. A simulation of the
+// reference (`MCTS.simulate`, blokus_rl/alphazero/mcts.py:13-71) is split into
+//   k_select        descent from the root (mcts.py:37-50) to a board not yet in the tree or a
+//                   terminal board, recording the path; writes the leaf's observation row and
+//                   legal bitmask (mcts.py:60-66) so the caller can batch every tree's leaf into
+//                   one policy/value forward pass;
+//   (the net)       PyTorch-ROCm forward on the [T, 2P, N, N] leaf batch;
+//   k_expand_backup expansion with P = exp(log_softmax(logp[legal ids]))
+//                   (neural_network.py:159-173, mcts.py:67-70) and the backup
+//                   Q <- (N*Q + v)/(N+1), N += 1 with v = scores[player to move at the child]
+//                   (mcts.py:53-56).
+// Each tree is touched by exactly one wave per kernel, so its table, node and child regions
+// need no atomics. All search arithmetic is float64 (the reference's pinned numpy 1.25 promotes
+// every float32 meeting a Python number to float64), compiled with -ffp-contract=off.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/blokus_engine.h"
+#include "ctx.h"
+
+namespace bk {
+
+constexpr int kMaxDepth = 96;  // > 84 = most placements a 4-player game can still make
+
+struct DevMcts {
+  int T, node_cap, TS;  // TS = table slots per tree (power of two)
+  int64_t child_cap_per_tree;
+  uint64_t* tab_key;    // [T*TS] 0 = empty
+  int32_t* tab_node;    // [T*TS] tree-local node index
+  int32_t* tree_nodes;  // [T]
+  int64_t* tree_children;  // [T] children used in the tree's region
+  int64_t* node_child;  // [T*node_cap] offset into the child arrays (global index)
+  int32_t* node_K;      // [T*node_cap]
+  uint32_t* node_visits;  // [T*node_cap]  = sum of the children's N
+  int32_t* ch_id;       // [T*cpt]
+  uint32_t* ch_N;
+  double* ch_Q;
+  float* ch_P;
+  int32_t* path_node;   // [T*kMaxDepth] tree-local node
+  int64_t* path_child;  // [T*kMaxDepth] global child index
+  int32_t* path_pl;     // [T*kMaxDepth] player to move at the child (scores index)
+  int32_t* depth;       // [T]
+  uint32_t* leaf_state; // [T*kStateWords]
+  int32_t* leaf_status; // [T]
+  double* leaf_scores;  // [T*kMaxP]
+  uint64_t* leaf_mask;  // [T*W64] internal copy of the leaf bitmask
+  unsigned long long* counters;  // [8]
+};
+
+enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5 };
+enum { kErrChildPool = 1, kErrTable = 2, kErrDepth = 4, kErrIllegal = 8, kErrMissingRoot = 16 };
+
+__device__ __forceinline__ uint64_t table_key(const uint32_t* s) {
+  const uint64_t h = state_hash(s);
+  return h ? h : 1ull;
+}
+
+// Wave-parallel linear probe; returns the tree-local node or -1 (key absent).
+__device__ __forceinline__ int table_find(const DevMcts& m, int t, uint64_t key, int* free_slot) {
+  const int l = lane_id();
+  const uint32_t mask = (uint32_t)m.TS - 1u;
+  const uint32_t start = (uint32_t)(key ^ (key >> 29)) & mask;
+  const uint64_t* keys = m.tab_key + (size_t)t * m.TS;
+  for (int p0 = 0; p0 < m.TS; p0 += kWave) {
+    const uint32_t slot = (start + (uint32_t)(p0 + l)) & mask;
+    const uint64_t k = keys[slot];
+    const uint64_t hit = __ballot(k == key);
+    const uint64_t emp = __ballot(k == 0ull);
+    if (hit) {
+      const int src = __ffsll((unsigned long long)hit) - 1;
+      const int slot_hit = __shfl((int)slot, src, kWave);
+      return m.tab_node[(size_t)t * m.TS + slot_hit];
+    }
+    if (emp) {
+      const int src = __ffsll((unsigned long long)emp) - 1;
+      if (free_slot) *free_slot = __shfl((int)slot, src, kWave);
+      return -1;
+    }
+  }
+  if (free_slot) *free_slot = -1;
+  return -1;
+}
+
+// argmax over (value, index): larger value wins, ties -> smaller index (np.argmax's first max).
+__device__ __forceinline__ void wave_argmax(double& best, int& bi) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o, kWave);
+    const int oi = __shfl_xor(bi, o, kWave);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+}
+
+// PUCT choice at a node (mcts.py:41-46): argmax_i Q_i + cpuct*P_i*sqrt(sum N + 1e-6)/(1+N_i).
+__device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, uint32_t visits, double cp) {
+  const int l = lane_id();
+  const double sq = sqrt((double)visits + 1e-6);
+  double best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = l; i < K; i += kWave) {
+    const double u = ((cp * (double)m.ch_P[off + i]) * sq) / (1.0 + (double)m.ch_N[off + i]);
+    const double hv = m.ch_Q[off + i] + u;
+    if (hv > best) { best = hv; bi = i; }
+  }
+  wave_argmax(best, bi);
+  return __shfl(bi, 0, kWave);
+}
+
+__global__ __launch_bounds__(64) void k_reset(DevMcts m, const int32_t* flags) {
+  const int t = blockIdx.y;
+  if (flags && !flags[t]) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m.TS) m.tab_key[(size_t)t * m.TS + i] = 0ull;
+  if (i == 0) { m.tree_nodes[t] = 0; m.tree_children[t] = 0; }
+}
+
+__global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
+                                               const int32_t* __restrict__ active, double cpuct,
+                                               int32_t* __restrict__ status_out, float* __restrict__ obs,
+                                               uint64_t* __restrict__ mask_out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* s = lds;
+  uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
+  uint32_t* m32 = lds + kStateWords + 2 * kMaxN;
+  const int t = blockIdx.x;
+  const int l = lane_id();
+  const int obs_len = 2 * dp.P * dp.N * dp.N;
+  if (active && !active[t]) {
+    if (l == 0) { m.leaf_status[t] = 0; status_out[t] = 0; m.depth[t] = 0; }
+    for (int i = l; i < obs_len; i += kWave) obs[(size_t)t * obs_len + i] = 0.0f;
+    return;
+  }
+  load_state(s, roots + (size_t)t * kStateWords);
+  __syncthreads();
+  double cp = cpuct;
+  int depth = 0, err = 0;
+  for (;;) {
+    const int node = table_find(m, t, table_key(s), nullptr);
+    if (node < 0) break;
+    const size_t gn = (size_t)t * m.node_cap + node;
+    const int64_t off = m.node_child[gn];
+    const int ci = select_child(m, off, m.node_K[gn], m.node_visits[gn], cp);
+    const int a = m.ch_id[off + ci];
+    if (depth >= kMaxDepth) { err |= kErrDepth; break; }
+    if (apply_action(dp, s, a, fa)) { err |= kErrIllegal; break; }
+    if (l == 0) {
+      const size_t pi = (size_t)t * kMaxDepth + depth;
+      m.path_node[pi] = node;
+      m.path_child[pi] = off + ci;
+      m.path_pl[pi] = (int)s[kWToMove];
+    }
+    ++depth;
+    cp = 1.0;  // the recursive call of mcts.py:50 passes no cpuct
+  }
+  int status;
+  float* o = obs + (size_t)t * obs_len;
+  if (err) {
+    status = 0;
+  } else if (s[kWFlags] & kFlagOver) {
+    status = 2;
+    if (l == 0) terminal_scores(dp, s, m.leaf_scores + (size_t)t * kMaxP);
+  } else {
+    status = 1;
+    build_mask(dp, s, (int)s[kWToMove], fa, m32);
+    uint64_t* mo = m.leaf_mask + (size_t)t * dp.W64;
+    uint64_t* mo2 = mask_out ? mask_out + (size_t)t * dp.W64 : nullptr;
+    for (int j = l; j < dp.W64; j += kWave) {
+      const uint64_t w = (uint64_t)m32[2 * j] | ((uint64_t)m32[2 * j + 1] << 32);
+      mo[j] = w;
+      if (mo2) mo2[j] = w;
+    }
+    store_state(m.leaf_state + (size_t)t * kStateWords, s);
+  }
+  // observation row (zeros unless the leaf needs the net)
+  const int NN = dp.N * dp.N;
+  const int tm = (int)s[kWToMove];
+  for (int i = l; i < obs_len; i += kWave) {
+    float v = 0.0f;
+    if (status == 1) {
+      const int plane = i / NN, cell = i - plane * NN;
+      if (plane < dp.P) {
+        const int r = cell / dp.N, c = cell - r * dp.N;
+        v = (float)((s[plane * kMaxN + r] >> c) & 1u);
+      } else {
+        v = (plane - dp.P) == tm ? 1.0f : 0.0f;
+      }
+    }
+    o[i] = v;
+  }
+  if (l == 0) {
+    m.leaf_status[t] = status;
+    status_out[t] = status;
+    m.depth[t] = depth;
+    atomicAdd(&m.counters[kCtrLevels], (unsigned long long)depth);
+    if (status == 2) atomicAdd(&m.counters[kCtrTerminal], 1ull);
+    if (err) atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
+  }
+}
+
+// prior_mode 0: logp = the net's log-probabilities over all A ids -> masked log-softmax + exp
+//               (get_valid_dist, neural_network.py:159-173);
+// prior_mode 1: logp holds the prior itself at the legal ids (test hook: identical P fed to the
+//               reference and to this engine).
+__global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, const float* __restrict__ logp,
+                                                      const float* __restrict__ values, int prior_mode) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* m32 = lds;  // W32pad words
+  __shared__ double vsh[kMaxP];
+  const int t = blockIdx.x;
+  const int l = lane_id();
+  const int status = m.leaf_status[t];
+  if (status == 0) return;
+  if (status == 1) {
+    const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
+    for (int j = l; j < dp.W64; j += kWave) {
+      const uint64_t w = lm[j];
+      m32[2 * j] = (uint32_t)w;
+      m32[2 * j + 1] = (uint32_t)(w >> 32);
+    }
+    __syncthreads();
+    int err = 0;
+    const int node = m.tree_nodes[t];
+    const int64_t used = m.tree_children[t];
+    const int64_t room = m.child_cap_per_tree - used;
+    const int64_t off = (int64_t)t * m.child_cap_per_tree + used;
+    // legal ids, ascending (np.where order, mcts.py:64), straight into the child region
+    const int K = compact_ids(dp, m32, m.ch_id + off, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
+    __syncthreads();
+    if (node >= m.node_cap) err |= kErrTable;
+    if (K > room) err |= kErrChildPool;
+    int free_slot = -1;
+    const uint64_t key = table_key(m.leaf_state + (size_t)t * kStateWords);
+    if (!err) {
+      const int found = table_find(m, t, key, &free_slot);
+      if (found >= 0 || free_slot < 0) err |= kErrTable;
+    }
+    if (!err) {
+      const float* lp = logp + (size_t)t * dp.A;
+      const int32_t* cid = m.ch_id + off;
+      if (prior_mode == 0) {
+        float mx = -INFINITY;
+        for (int i = l; i < K; i += kWave) mx = fmaxf(mx, lp[cid[i]]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, kWave));
+        float sum = 0.0f;
+        for (int i = l; i < K; i += kWave) sum += expf(lp[cid[i]] - mx);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+        const float lse = logf(sum);
+        for (int i = l; i < K; i += kWave) {
+          m.ch_N[off + i] = 0u;
+          m.ch_Q[off + i] = 0.0;
+          m.ch_P[off + i] = expf((lp[cid[i]] - mx) - lse);
+        }
+      } else {
+        for (int i = l; i < K; i += kWave) {
+          m.ch_N[off + i] = 0u;
+          m.ch_Q[off + i] = 0.0;
+          m.ch_P[off + i] = lp[cid[i]];
+        }
+      }
+      if (l == 0) {
+        const size_t gn = (size_t)t * m.node_cap + node;
+        m.node_child[gn] = off;
+        m.node_K[gn] = K;
+        m.node_visits[gn] = 0u;
+        m.tab_key[(size_t)t * m.TS + free_slot] = key;
+        m.tab_node[(size_t)t * m.TS + free_slot] = node;
+        m.tree_nodes[t] = node + 1;
+        m.tree_children[t] = used + K;
+        atomicAdd(&m.counters[kCtrExpanded], 1ull);
+      }
+    } else if (l == 0) {
+      atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
+    }
+    if (l < dp.P) vsh[l] = (double)values[(size_t)t * dp.P + l];
+  } else {
+    if (l < dp.P) vsh[l] = m.leaf_scores[(size_t)t * kMaxP + l];
+  }
+  __syncthreads();
+  const int depth = m.depth[t];
+  for (int d = l; d < depth; d += kWave) {
+    const size_t pi = (size_t)t * kMaxDepth + d;
+    const int64_t ci = m.path_child[pi];
+    const double v = vsh[m.path_pl[pi]];
+    const uint32_t n = m.ch_N[ci];
+    const double q = m.ch_Q[ci];
+    m.ch_Q[ci] = ((double)n * q + v) / (double)(n + 1u);
+    m.ch_N[ci] = n + 1u;
+    m.node_visits[(size_t)t * m.node_cap + m.path_node[pi]] += 1u;
+  }
+}
+
+// get_distribution (mcts.py:73-99) / root statistics. mode 0 -> pi, mode 1 -> raw stats.
+__global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restrict__ roots,
+                                             const int32_t* __restrict__ active, double temperature, int mode,
+                                             int32_t* ids, double* pi, uint32_t* n_out, double* q_out, float* p_out,
+                                             int cap, int32_t* counts) {
+  const int t = blockIdx.x;
+  const int l = lane_id();
+  if (active && !active[t]) {
+    if (l == 0) counts[t] = 0;
+    return;
+  }
+  const uint32_t* s = roots + (size_t)t * kStateWords;
+  const uint64_t key = table_key(s);
+  const int node = table_find(m, t, key, nullptr);
+  if (node < 0) {
+    if (l == 0) { counts[t] = -1; atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrMissingRoot); }
+    return;
+  }
+  const size_t gn = (size_t)t * m.node_cap + node;
+  const int64_t off = m.node_child[gn];
+  const int K = m.node_K[gn];
+  if (l == 0) counts[t] = K <= cap ? K : -K;
+  const int Kc = K <= cap ? K : cap;
+  if (mode == 1) {
+    for (int i = l; i < Kc; i += kWave) {
+      ids[(size_t)t * cap + i] = m.ch_id[off + i];
+      n_out[(size_t)t * cap + i] = m.ch_N[off + i];
+      q_out[(size_t)t * cap + i] = m.ch_Q[off + i];
+      p_out[(size_t)t * cap + i] = m.ch_P[off + i];
+    }
+    return;
+  }
+  for (int i = l; i < Kc; i += kWave) ids[(size_t)t * cap + i] = m.ch_id[off + i];
+  double* o = pi + (size_t)t * cap;
+  if (temperature == 0.0) {
+    // 1/0 raises ZeroDivisionError in the reference -> one-hot at the first max of N
+    double best = -1.0;
+    int bi = 0x7fffffff;
+    for (int i = l; i < K; i += kWave) {
+      const double v = (double)m.ch_N[off + i];
+      if (v > best) { best = v; bi = i; }
+    }
+    wave_argmax(best, bi);
+    bi = __shfl(bi, 0, kWave);
+    for (int i = l; i < Kc; i += kWave) o[i] = i == bi ? 1.0 : 0.0;
+    return;
+  }
+  // N^(1/T), summed left to right like Python's object-array sum, then normalised.
+  const double e = 1.0 / temperature;
+  for (int i = l; i < Kc; i += kWave) o[i] = pow((double)m.ch_N[off + i], e);
+  __syncthreads();
+  if (l == 0) {
+    double total = 0.0;
+    for (int i = 0; i < K; ++i) total += (i < Kc) ? o[i] : pow((double)m.ch_N[off + i], e);
+    if (total == 0.0) {
+      for (int i = 0; i < Kc; ++i) o[i] = 1.0 / (double)K;
+    } else {
+      for (int i = 0; i < Kc; ++i) o[i] = o[i] / total;
+    }
+  }
+}
+
+}  // namespace bk
+
+using namespace bk;
+
+struct bk_mcts {
+  bk_ctx* ctx = nullptr;
+  DevMcts d{};
+  std::vector<void*> allocs;
+};
+
+template <typename T>
+static int mcts_alloc(bk_mcts* m, T** p, size_t count) {
+  void* q = nullptr;
+  int rc = hip_check(hipMalloc(&q, sizeof(T) * (count ? count : 1)), "hipMalloc mcts");
+  if (rc) return rc;
+  m->allocs.push_back(q);
+  *p = (T*)q;
+  return BK_OK;
+}
+
+extern "C" {
+
+int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_mcts** out) {
+  BK_REQUIRE(ctx && out && trees > 0 && node_cap > 0 && child_cap >= trees, "bad argument");
+  BK_REQUIRE(ctx->d_items, "host-only context (created with device < 0)");
+  *out = nullptr;
+  bk_mcts* m = new bk_mcts();
+  m->ctx = ctx;
+  DevMcts& d = m->d;
+  d.T = trees;
+  d.node_cap = node_cap;
+  int TS = 64;
+  while (TS < 2 * node_cap) TS <<= 1;
+  d.TS = TS;
+  d.child_cap_per_tree = child_cap / trees;
+  const size_t T = (size_t)trees;
+  const int W64 = ctx->dp.W64;
+  int rc = hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+  if (!rc) rc = mcts_alloc(m, &d.tab_key, T * TS);
+  if (!rc) rc = mcts_alloc(m, &d.tab_node, T * TS);
+  if (!rc) rc = mcts_alloc(m, &d.tree_nodes, T);
+  if (!rc) rc = mcts_alloc(m, &d.tree_children, T);
+  if (!rc) rc = mcts_alloc(m, &d.node_child, T * node_cap);
+  if (!rc) rc = mcts_alloc(m, &d.node_K, T * node_cap);
+  if (!rc) rc = mcts_alloc(m, &d.node_visits, T * node_cap);
+  const size_t C = (size_t)d.child_cap_per_tree * T;
+  if (!rc) rc = mcts_alloc(m, &d.ch_id, C);
+  if (!rc) rc = mcts_alloc(m, &d.ch_N, C);
+  if (!rc) rc = mcts_alloc(m, &d.ch_Q, C);
+  if (!rc) rc = mcts_alloc(m, &d.ch_P, C);
+  if (!rc) rc = mcts_alloc(m, &d.path_node, T * kMaxDepth);
+  if (!rc) rc = mcts_alloc(m, &d.path_child, T * kMaxDepth);
+  if (!rc) rc = mcts_alloc(m, &d.path_pl, T * kMaxDepth);
+  if (!rc) rc = mcts_alloc(m, &d.depth, T);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_state, T * kStateWords);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_status, T);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_scores, T * kMaxP);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_mask, T * W64);
+  if (!rc) rc = mcts_alloc(m, &d.counters, 8);
+  if (!rc) rc = hip_check(hipMemset(d.counters, 0, 8 * sizeof(unsigned long long)), "memset counters");
+  if (!rc) rc = hip_check(hipMemset(d.leaf_status, 0, T * sizeof(int32_t)), "memset status");
+  if (!rc) rc = hip_check(hipMemset(d.depth, 0, T * sizeof(int32_t)), "memset depth");
+  if (rc) { bk_mcts_destroy(m); return rc; }
+  rc = bk_mcts_reset(m, nullptr, nullptr);
+  if (!rc) rc = hip_check(hipDeviceSynchronize(), "sync");
+  if (rc) { bk_mcts_destroy(m); return rc; }
+  *out = m;
+  return BK_OK;
+}
+
+int bk_mcts_destroy(bk_mcts* m) {
+  if (!m) return BK_OK;
+  for (void* p : m->allocs) (void)hipFree(p);
+  delete m;
+  return BK_OK;
+}
+
+int bk_mcts_reset(bk_mcts* m, const int32_t* reset_flags, void* stream) {
+  BK_REQUIRE(m, "null mcts");
+  hipLaunchKernelGGL(k_reset, dim3((m->d.TS + 63) / 64, m->d.T), dim3(64), 0, (hipStream_t)stream, m->d,
+                     reset_flags);
+  return launch_check("k_reset");
+}
+
+int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int32_t* leaf_status,
+                   float* obs, uint64_t* leaf_mask, void* stream) {
+  BK_REQUIRE(m && roots && leaf_status && obs, "bad argument");
+  const DevPreset& dp = m->ctx->dp;
+  const size_t lds = sizeof(uint32_t) * (size_t)(kStateWords + 2 * kMaxN + dp.W32pad);
+  hipLaunchKernelGGL(k_select, dim3(m->d.T), dim3(kWave), lds, (hipStream_t)stream, dp, m->d,
+                     (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask);
+  return launch_check("k_select");
+}
+
+int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, int prior_mode, void* stream) {
+  BK_REQUIRE(m && logp && values && (prior_mode == 0 || prior_mode == 1), "bad argument");
+  const DevPreset& dp = m->ctx->dp;
+  const size_t lds = sizeof(uint32_t) * (size_t)dp.W32pad;
+  hipLaunchKernelGGL(k_expand_backup, dim3(m->d.T), dim3(kWave), lds, (hipStream_t)stream, dp, m->d, logp, values,
+                     prior_mode);
+  return launch_check("k_expand_backup");
+}
+
+int bk_mcts_root_policy(bk_mcts* m, const void* roots, const int32_t* active, double temperature, int32_t* ids,
+                        double* pi, int cap, int32_t* counts, void* stream) {
+  BK_REQUIRE(m && roots && ids && pi && counts && cap > 0 && temperature >= 0.0, "bad argument");
+  hipLaunchKernelGGL(k_root, dim3(m->d.T), dim3(kWave), 0, (hipStream_t)stream, m->d, (const uint32_t*)roots,
+                     active, temperature, 0, ids, pi, (uint32_t*)nullptr, (double*)nullptr, (float*)nullptr, cap,
+                     counts);
+  return launch_check("k_root policy");
+}
+
+int bk_mcts_root_stats(bk_mcts* m, const void* roots, const int32_t* active, int32_t* ids, uint32_t* n, double* q,
+                       float* p, int cap, int32_t* counts, void* stream) {
+  BK_REQUIRE(m && roots && ids && n && q && p && counts && cap > 0, "bad argument");
+  hipLaunchKernelGGL(k_root, dim3(m->d.T), dim3(kWave), 0, (hipStream_t)stream, m->d, (const uint32_t*)roots,
+                     active, 1.0, 1, ids, (double*)nullptr, n, q, p, cap, counts);
+  return launch_check("k_root stats");
+}
+
+int bk_mcts_leaf_info(bk_mcts* m, void* leaf_states, int32_t* depths, void* stream) {
+  BK_REQUIRE(m && leaf_states && depths, "bad argument");
+  int rc = hip_check(hipMemcpyAsync(leaf_states, m->d.leaf_state, (size_t)m->d.T * kStateBytes,
+                                    hipMemcpyDeviceToDevice, (hipStream_t)stream), "copy leaf states");
+  if (!rc) rc = hip_check(hipMemcpyAsync(depths, m->d.depth, (size_t)m->d.T * sizeof(int32_t),
+                                         hipMemcpyDeviceToDevice, (hipStream_t)stream), "copy depths");
+  return rc;
+}
+
+int bk_mcts_counters(bk_mcts* m, int64_t* out, void* stream) {
+  BK_REQUIRE(m && out, "bad argument");
+  unsigned long long c[8];
+  int rc = hip_check(hipMemcpyAsync(c, m->d.counters, sizeof(c), hipMemcpyDeviceToHost, (hipStream_t)stream),
+                     "copy counters");
+  if (!rc) rc = hip_check(hipStreamSynchronize((hipStream_t)stream), "sync counters");
+  if (rc) return rc;
+  std::vector<int32_t> nodes(m->d.T);
+  std::vector<int64_t> ch(m->d.T);
+  rc = hip_check(hipMemcpy(nodes.data(), m->d.tree_nodes, sizeof(int32_t) * m->d.T, hipMemcpyDeviceToHost),
+                 "copy nodes");
+  if (!rc) rc = hip_check(hipMemcpy(ch.data(), m->d.tree_children, sizeof(int64_t) * m->d.T,
+                                    hipMemcpyDeviceToHost), "copy children");
+  if (rc) return rc;
+  int64_t tn = 0, tc = 0;
+  for (int t = 0; t < m->d.T; ++t) { tn += nodes[t]; tc += ch[t]; }
+  out[0] = tn;
+  out[1] = tc;
+  for (int k = 2; k < 8; ++k) out[k] = (int64_t)c[k];
+  return BK_OK;
+}
+
+}  // extern "C"

@@ -62,6 +62,7 @@ int bk_state_bytes(void);
  * board_size N (5..20), num_players P (2 or 4), max_piece_cells (1..5).
  * Presets used by the reference: (20,4,5) -> 30433 actions (docs/README.md:128);
  * (7,2,4) -> 919 actions (docs/README.md:51); (7,2,5) -> 2522 (the 7x7 recordings).
+ * device < 0 creates a host-only context (tables only; every device call then fails).
  * Replaces: BlokusEnvironment() + _set_all_possible_moves (blokus_wrapper.py:42, :281-324). */
 int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int device, bk_ctx** out);
 int bk_ctx_destroy(bk_ctx* ctx);
@@ -122,7 +123,7 @@ int bk_legal_ids(bk_ctx* ctx, const void* states, const int32_t* players, int B,
  * transposition table keyed by the board hash (mcts.py:37-39) with SoA child statistics
  * {id, N, Q (f64), P (f32)}; it persists across moves of one game (trainer.py:95).
  *   node_cap  : nodes per tree (hash table sized to 2x that, power of two)
- *   child_cap : children in the shared pool across all trees */
+ *   child_cap : total child slots, split evenly into one region per tree */
 int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_mcts** out);
 int bk_mcts_destroy(bk_mcts* m);
 /* Clear the trees whose flag is non-zero (reset_flags: [T] int32 device, NULL = all):
@@ -143,7 +144,10 @@ int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double 
  * P = exp(log_softmax(logp[t][legal ids])) (neural_network.py:159-173) and back up
  * values[t][P]; for status-2 leaves back up the terminal scores. logp: [T][A] f32 (the net's
  * log-softmax output, rows of inactive/terminal trees ignored); values: [T][P] f32. */
-int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, void* stream);
+int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, int prior_mode,
+                          void* stream);
+/* prior_mode 1 (test hook): logp[t][id] already holds the prior P at the legal ids; no softmax.
+ * Lets a test feed the reference MCTS and this engine identical priors. */
 
 /* get_distribution (mcts.py:73-99) at the root of every active tree: ids[t][0..K) and
  * pi[t][0..K) (f64) in child order, K in counts[t]; temperature 0 -> one-hot argmax N
@@ -154,6 +158,9 @@ int bk_mcts_root_policy(bk_mcts* m, const void* roots, const int32_t* active, do
 /* Root child statistics (for tests / players): n[t][cap] u32, q[t][cap] f64, p[t][cap] f32. */
 int bk_mcts_root_stats(bk_mcts* m, const void* roots, const int32_t* active, int32_t* ids,
                        uint32_t* n, double* q, float* p, int cap, int32_t* counts, void* stream);
+
+/* Leaf of the last select pass, per tree: leaf_states [T][384] (device), depths [T] int32. */
+int bk_mcts_leaf_info(bk_mcts* m, void* leaf_states, int32_t* depths, void* stream);
 
 /* Engine counters (host copy, synchronises the stream): out[0] nodes used (all trees),
  * out[1] children used, out[2] selection levels descended (cumulative), out[3] leaves
