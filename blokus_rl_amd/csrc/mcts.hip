@@ -294,6 +294,11 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
   }
 }
 
+__device__ __forceinline__ double raise_visits(uint32_t n, double e) {
+  if (e == 1.0 || n <= 1u) return (double)n;
+  return pow((double)n, e);
+}
+
 // get_distribution (mcts.py:73-99) / root statistics. mode 0 -> pi, mode 1 -> raw stats.
 __global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restrict__ roots,
                                              const int32_t* __restrict__ active, double temperature, int mode,
@@ -342,12 +347,14 @@ __global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restri
     return;
   }
   // N^(1/T), summed left to right like Python's object-array sum, then normalised.
+  // N^1 is exact in the reference (int ** 1.0); device pow() is not correctly rounded, so the
+  // default temperature 1 bypasses it. Other temperatures agree to ~1 ulp with host libm.
   const double e = 1.0 / temperature;
-  for (int i = l; i < Kc; i += kWave) o[i] = pow((double)m.ch_N[off + i], e);
+  for (int i = l; i < Kc; i += kWave) o[i] = raise_visits(m.ch_N[off + i], e);
   __syncthreads();
   if (l == 0) {
     double total = 0.0;
-    for (int i = 0; i < K; ++i) total += (i < Kc) ? o[i] : pow((double)m.ch_N[off + i], e);
+    for (int i = 0; i < K; ++i) total += (i < Kc) ? o[i] : raise_visits(m.ch_N[off + i], e);
     if (total == 0.0) {
       for (int i = 0; i < Kc; ++i) o[i] = 1.0 / (double)K;
     } else {

@@ -192,6 +192,7 @@ class MCTSOracle:
         self.o = oracle
         self.evaluate = evaluate
         self.tree: dict[int, dict] = {}
+        self.terminal_hits = 0
 
     def simulate(self, s: np.ndarray, cpuct: float = 1.0):
         h = self.o.hash(s)
@@ -215,6 +216,7 @@ class MCTSOracle:
             return scores
         ended = self.o.game_ended(s)  # mcts.py:59-61
         if ended is not None:
+            self.terminal_hits += 1
             return ended
         ids, p, v = self.evaluate(s, player)
         self.tree[h] = {
