@@ -190,6 +190,11 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--games", type=int, default=256)
+    ap.add_argument("--sims", type=int, default=100)
+    ap.add_argument("--model", default="resnet", choices=["resnet", "dumbnet", "dcnnet"])
+    ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--node-cap", type=int, default=8192)
     args = ap.parse_args()
     world, rank, _ = _dist_init()
     if args.workload == "legal":
@@ -197,6 +202,7 @@ def main():
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay
         out = bench_selfplay(args, world, rank)
+        out.pop("_selfplay", None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

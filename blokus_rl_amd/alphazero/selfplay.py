@@ -1,0 +1,244 @@
+"""GPU self-play: G concurrent games, one batched search tree per game.
+
+Restates `AlphaZeroTrainer._self_play` (blokus_rl/alphazero/trainer.py:92-137) for G games at
+once, every step on the device:
+  per ply: `num_sims` x { k_select -> net forward on the [G, 2P, N, N] leaf batch ->
+           k_expand_backup }, then get_distribution(T) at the root (mcts.py:73-99), root-only
+           Dirichlet(alpha=1) mixing 0.75/0.25 on a game's first ply (trainer.py:110-116),
+           sampling from pi (trainer.py:124-125), recording (state, pi, player), next state.
+  at game end: every example of the game gets z = the final one-hot scores (trainer.py:134-135).
+The host only launches; random numbers come from torch's device generator (per-run seed), so
+trajectories are statistically — not stream-for-stream — equivalent to np.random's.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..engine import Engine
+from .batched_mcts import BatchedMCTS
+
+
+@dataclass
+class Examples:
+    """Packed replay examples (the all-gathered (s, pi, z) of SURVEY.md §8e): fixed stride."""
+    states: torch.Tensor  # [E, 384] u8 — the root state (observation and mask are recomputed)
+    ids: torch.Tensor     # [E, cap] int16 — legal ids of pi (ascending), -1 padded
+    pi: torch.Tensor      # [E, cap] f32 — MCTS policy over ids
+    k: torch.Tensor       # [E] int32 — number of ids
+    z: torch.Tensor       # [E, P] f32 — final scores of the game (-1 / 3 / 1)
+
+    def __len__(self):
+        return int(self.states.shape[0])
+
+
+@dataclass
+class SelfPlayStats:
+    sims: int = 0
+    plies: int = 0
+    games_finished: int = 0
+    seconds: float = 0.0
+    nn_seconds: float = 0.0
+    extra: dict = field(default_factory=dict)
+
+
+class LeafEvaluator:
+    """Wraps the policy/value net for the leaf batch: obs [G, 2P, N, N] -> (logp [G, A] f32,
+    v [G, P] f32). DumbNet needs no forward: a constant uniform log-prior and zero values."""
+
+    def __init__(self, model: torch.nn.Module | None, eng: Engine, G: int, dtype: torch.dtype = torch.float32,
+                 use_graph: bool = True):
+        self.model = model
+        self.eng = eng
+        self.G = G
+        self.dtype = dtype
+        dev = eng.device
+        self.const_logp = None
+        if model is None or model.__class__.__name__ == "DumbNet":
+            self.const_logp = torch.full((G, eng.A), -float(torch.log(torch.tensor(float(eng.A)))),
+                                         dtype=torch.float32, device=dev)
+            self.const_v = torch.zeros((G, eng.P), dtype=torch.float32, device=dev)
+            self.model = None
+            return
+        self.model.eval()
+        self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32, device=dev)
+        self.graph = None
+        if use_graph:
+            self._capture()
+
+    def _forward(self, obs):
+        with torch.inference_mode():
+            if self.dtype != torch.float32:
+                with torch.autocast("cuda", dtype=self.dtype):
+                    lp, v = self.model(obs)
+            else:
+                lp, v = self.model(obs)
+            return lp.float().contiguous(), v.float().contiguous()
+
+    def _capture(self):
+        s = torch.cuda.Stream(self.eng.device)
+        s.wait_stream(torch.cuda.current_stream(self.eng.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._forward(self.static_obs)
+        torch.cuda.current_stream(self.eng.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.static_lp, self.static_v = self._forward(self.static_obs)
+        self.graph = g
+
+    def __call__(self, obs: torch.Tensor):
+        if self.model is None:
+            return self.const_logp, self.const_v
+        if self.graph is not None:
+            self.static_obs.copy_(obs)
+            self.graph.replay()
+            return self.static_lp, self.static_v
+        return self._forward(obs)
+
+
+class SelfPlay:
+    def __init__(self, eng: Engine, model: torch.nn.Module | None, games: int, num_sims: int = 100,
+                 cpuct: float = 1.0, temperature: float = 1.0, dirichlet_alpha: float = 1.0,
+                 dirichlet_weight: float = 0.25, node_cap: int = 8192, child_cap: int | None = None,
+                 cap: int = 2048, seed: int = 0, nn_dtype: torch.dtype = torch.float32, use_graph: bool = True,
+                 continuous: bool = False):
+        self.eng = eng
+        self.G = games
+        self.num_sims = num_sims
+        self.cpuct = cpuct
+        self.temperature = temperature
+        self.alpha = dirichlet_alpha
+        self.weight = dirichlet_weight
+        self.cap = cap
+        self.continuous = continuous
+        self.mcts = BatchedMCTS(eng, games, node_cap=node_cap, child_cap=child_cap)
+        self.evaluator = LeafEvaluator(model, eng, games, nn_dtype, use_graph)
+        dev = eng.device
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed)
+        self.roots = eng.init_states(games)
+        self.active = torch.ones(games, dtype=torch.int32, device=dev)
+        self.first_ply = torch.ones(games, dtype=torch.bool, device=dev)
+        self.game_id = torch.arange(games, dtype=torch.int64, device=dev)
+        self.next_game_id = games
+        self.stats = SelfPlayStats()
+        self._pending: list[tuple[torch.Tensor, ...]] = []  # per-ply records awaiting z
+        self.timers = None
+        self.finished: list[Examples] = []
+
+    # ------------------------------------------------------------------ one simulation
+    def simulate(self):
+        """One simulation in every active tree (= num active trees simulate() calls)."""
+        if self.timers is not None:
+            return self._simulate_timed()
+        _, obs, _ = self.mcts.select(self.roots, self.active, self.cpuct)
+        logp, v = self.evaluator(obs)
+        self.mcts.expand_backup(logp, v, prior_mode=0)
+
+    def enable_timers(self, on: bool = True):
+        """HIP events around each stage on the launch stream (bench.py roofline inputs)."""
+        self.timers = {"select": [], "net": [], "expand": []} if on else None
+
+    def _simulate_timed(self):
+        st = torch.cuda.current_stream(self.eng.device)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(st)
+        _, obs, _ = self.mcts.select(self.roots, self.active, self.cpuct)
+        ev[1].record(st)
+        logp, v = self.evaluator(obs)
+        ev[2].record(st)
+        self.mcts.expand_backup(logp, v, prior_mode=0)
+        ev[3].record(st)
+        self.timers["select"].append((ev[0], ev[1]))
+        self.timers["net"].append((ev[1], ev[2]))
+        self.timers["expand"].append((ev[2], ev[3]))
+
+    def timer_ms(self) -> dict:
+        torch.cuda.synchronize(self.eng.device)
+        return {k: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else 0.0) for k, v in self.timers.items()}
+
+    # ------------------------------------------------------------------ one ply
+    def play_ply(self, record: bool = True):
+        for _ in range(self.num_sims):
+            self.simulate()
+        ids, pi, counts = self.mcts.root_policy(self.roots, self.active, self.temperature, self.cap)
+        G, cap = self.G, self.cap
+        col = torch.arange(cap, device=self.eng.device).unsqueeze(0)
+        valid = col < counts.clamp(min=0).unsqueeze(1)
+        pi = torch.where(valid, pi, torch.zeros_like(pi))
+        # root-only Dirichlet noise on each game's first ply (trainer.py:110-116)
+        if bool(self.first_ply.any()):
+            gam = torch._standard_gamma(torch.full((G, cap), self.alpha, dtype=torch.float64,
+                                                   device=self.eng.device), generator=self.gen)
+            gam = torch.where(valid, gam, torch.zeros_like(gam))
+            noise = gam / gam.sum(dim=1, keepdim=True).clamp(min=1e-300)
+            mixed = pi * (1 - self.weight) + noise * self.weight
+            pi = torch.where(self.first_ply.unsqueeze(1), mixed, pi)
+        pi32 = pi.to(torch.float32)
+        act_mask = self.active.bool() & (counts > 0)
+        probs = torch.where(act_mask.unsqueeze(1), pi32, (col == 0).to(torch.float32))
+        idx = torch.multinomial(probs, 1, generator=self.gen).view(-1)
+        action = ids.gather(1, idx.view(-1, 1)).view(-1)
+        action = torch.where(act_mask, action, torch.full_like(action, -1)).to(torch.int32).contiguous()
+        if record:
+            player = Engine.to_move(self.roots).clone()
+            self._pending.append((self.roots.clone(), ids.to(torch.int16), pi32, counts.clone(), player,
+                                  self.game_id.clone(), act_mask.clone()))
+        self.roots, _, status = self.eng.next_state(self.roots, action)
+        self.first_ply &= ~act_mask
+        self.stats.plies += 1
+        self.stats.sims += int(self.num_sims) * int(act_mask.sum().item())
+        ended, scores = self.eng.game_ended(self.roots)
+        done = ended.bool() & self.active.bool()
+        if bool(done.any()):
+            self._finish(done, scores)
+        return status
+
+    def _finish(self, done: torch.Tensor, scores: torch.Tensor):
+        """Assign z to every pending example of the finished games; reset/restart their trees."""
+        self.stats.games_finished += int(done.sum().item())
+        fin_ids = self.game_id[done]
+        z_of = {}
+        for gid, sc in zip(fin_ids.tolist(), scores[done].float()):
+            z_of[gid] = sc
+        keep = []
+        for rec in self._pending:
+            states, ids, pi, k, player, gids, m = rec
+            sel = m & torch.isin(gids, fin_ids)
+            if bool(sel.any()):
+                zs = torch.stack([z_of[g] for g in gids[sel].tolist()])
+                self.finished.append(Examples(states[sel], ids[sel], pi[sel], k[sel], zs))
+                m = m & ~sel
+            if bool(m.any()):
+                keep.append((states, ids, pi, k, player, gids, m))
+        self._pending = keep
+        flags = done.to(torch.int32)
+        self.mcts.reset(flags)  # a new MCTS per episode (trainer.py:95)
+        if self.continuous:
+            fresh = self.eng.init_states(self.G)
+            self.roots = torch.where(done.unsqueeze(1), fresh, self.roots)
+            self.first_ply |= done
+            n = int(done.sum().item())
+            self.game_id[done] = torch.arange(self.next_game_id, self.next_game_id + n, device=self.eng.device)
+            self.next_game_id += n
+        else:
+            self.active = self.active & ~flags
+
+    def run(self, plies: int):
+        t0 = time.perf_counter()
+        for _ in range(plies):
+            if not bool(self.active.any()):
+                break
+            self.play_ply()
+        torch.cuda.synchronize(self.eng.device)
+        self.stats.seconds += time.perf_counter() - t0
+        return self.stats
+
+    def examples(self) -> Examples | None:
+        if not self.finished:
+            return None
+        return Examples(*(torch.cat([getattr(e, f) for e in self.finished]) for f in
+                          ("states", "ids", "pi", "k", "z")))

@@ -1,0 +1,109 @@
+"""Policy/value nets used as the MCTS leaf evaluator, kept on PyTorch-ROCm (MIOpen convs,
+hipBLASLt GEMMs): the north star keeps the repo's existing net. Architectures, forward
+semantics and `state_dict` keys follow the reference so its checkpoints load unchanged:
+
+* `ResNet`  — blokus_rl/models/blokus_nnet.py:88-151: conv3x3(2P->64)+BN+ReLU, ONE residual
+  around the whole stack of `num_res_blocks` (conv-BN-ReLU-conv-BN) blocks, policy head
+  1x1 conv(2)+BN+ReLU+Linear(2*N*N -> A)+log_softmax, value head 1x1 conv(1)+BN+ReLU+
+  Linear(N*N -> 64)+ReLU+Linear(64 -> P)+tanh.
+* `DCNNet`  — blokus_nnet.py:9-85.
+* `DumbNet` — models/dumbnet.py:6-21: logits 1, value 0 (the "uninformed MCTS" opponent).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+class ResNet(nn.Module):
+    def __init__(self, board_size: int, num_players: int, action_size: int, num_res_blocks: int = 5,
+                 channels: int = 64):
+        super().__init__()
+        self.board_x = self.board_y = board_size
+        self.action_size = action_size
+        self.num_players = num_players
+        self.input_dim = [2 * num_players, board_size, board_size]
+        c = channels
+        self.conv1 = nn.Conv2d(2 * num_players, c, kernel_size=3, padding=1)
+        self.bn1 = nn.BatchNorm2d(c)
+        self.res_blocks = nn.Sequential(*[
+            nn.Sequential(nn.Conv2d(c, c, 3, padding=1), nn.BatchNorm2d(c), nn.ReLU(),
+                          nn.Conv2d(c, c, 3, padding=1), nn.BatchNorm2d(c))
+            for _ in range(num_res_blocks)
+        ])
+        n2 = board_size * board_size
+        self.policy_conv = nn.Conv2d(c, 2, kernel_size=1)
+        self.policy_bn = nn.BatchNorm2d(2)
+        self.policy_out = nn.Linear(2 * n2, action_size)
+        self.value_conv = nn.Conv2d(c, 1, kernel_size=1)
+        self.value_bn = nn.BatchNorm2d(1)
+        self.value_fc1 = nn.Linear(n2, 64)
+        self.value_fc2 = nn.Linear(64, num_players)
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)))
+        x = F.relu(x + self.res_blocks(x))
+        p = F.relu(self.policy_bn(self.policy_conv(x))).flatten(1)
+        p = F.log_softmax(self.policy_out(p), dim=1)
+        v = F.relu(self.value_bn(self.value_conv(x))).flatten(1)
+        v = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
+        return p, v
+
+
+class DCNNet(nn.Module):
+    def __init__(self, board_size: int, num_players: int, action_size: int, num_channels: int = 128,
+                 linear_dim: int = 128, dropout: float = 0.3):
+        super().__init__()
+        n, c, d = board_size, num_channels, linear_dim
+        self.num_channels, self.board_x, self.board_y, self.dropout = c, n, n, dropout
+        self.conv1 = nn.Conv2d(2 * num_players, c, 3, stride=1, padding=1)
+        self.conv2 = nn.Conv2d(c, c, 3, stride=1, padding=1)
+        self.conv3 = nn.Conv2d(c, c, 3, stride=1)
+        self.conv4 = nn.Conv2d(c, c, 3, stride=1)
+        self.bn1, self.bn2, self.bn3, self.bn4 = (nn.BatchNorm2d(c) for _ in range(4))
+        self.fc1 = nn.Linear(c * (n - 4) * (n - 4), d)
+        self.fc_bn1 = nn.BatchNorm1d(d)
+        self.fc2 = nn.Linear(d, d // 2)
+        self.fc_bn2 = nn.BatchNorm1d(d // 2)
+        self.fc3 = nn.Linear(d // 2, action_size)
+        self.fc4 = nn.Linear(d // 2, num_players)
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)))
+        x = F.relu(self.bn2(self.conv2(x)))
+        x = F.relu(self.bn3(self.conv3(x)))
+        x = F.relu(self.bn4(self.conv4(x)))
+        x = x.reshape(-1, self.num_channels * (self.board_x - 4) * (self.board_y - 4))
+        x = F.dropout(F.relu(self.fc_bn1(self.fc1(x))), p=self.dropout, training=self.training)
+        x = F.dropout(F.relu(self.fc_bn2(self.fc2(x))), p=self.dropout, training=self.training)
+        return F.log_softmax(self.fc3(x), dim=1), torch.tanh(self.fc4(x))
+
+
+class DumbNet(nn.Module):
+    """Uniform prior, zero value. Returns logits of 1 exactly like the reference (not a
+    log-softmax); the masked log-softmax downstream makes the prior uniform either way."""
+
+    def __init__(self, board_size: int, num_players: int, action_size: int):
+        super().__init__()
+        self.p_shape, self.v_shape = action_size, num_players
+
+    def forward(self, x):
+        b = x.shape[0]
+        return (torch.ones((b, self.p_shape), device=x.device),
+                torch.zeros((b, self.v_shape), device=x.device))
+
+
+def get_model(model_type: str):
+    """models/__init__.py:5-11 registry."""
+    return {"dumbnet": DumbNet, "dcnnet": DCNNet, "resnet": ResNet}[model_type]
+
+
+def build_model(model_type: str, board_size: int, num_players: int, action_size: int, **kw) -> nn.Module:
+    cls = get_model(model_type)
+    if cls is ResNet:
+        return ResNet(board_size, num_players, action_size, num_res_blocks=kw.get("num_res_blocks", 5))
+    if cls is DCNNet:
+        return DCNNet(board_size, num_players, action_size, kw.get("num_channels", 128), kw.get("linear_dim", 128),
+                      kw.get("dropout", 0.3))
+    return DumbNet(board_size, num_players, action_size)

