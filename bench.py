@@ -57,6 +57,14 @@ def _max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
+def _sum_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
 def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
     if one exists for this kernel; FETCH_SIZE doubled per the gfx950 correction
@@ -159,6 +167,7 @@ def bench_legal(args, world, rank):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_legal(states, args.cpu_seconds)
+    out["_states"] = states
     return out
 
 
@@ -179,12 +188,57 @@ def cpu_baseline_legal(states: torch.Tensor, seconds: float):
             "sample": f"{n} board evaluations (first 256 benchmark boards, repeated) in {dt:.1f} s"}
 
 
+def cpu_baseline_selfplay(seconds: float, model_type: str = "resnet"):
+    """Reference-equivalent CPU path: the pure-Python restatement of
+    MCTS.simulate (oracle/oracle.py, float64, dict-keyed tree), the C oracle env on 1 host core,
+    and — for resnet — batch-1 leaf evaluation of the unfused ResNet on the GPU with a host
+    round trip per leaf exactly like BlokusNNetWrapper.predict (neural_network.py:92-110).
+    One game from the empty board, 100 simulations per move, argmax moves, until `seconds`."""
+    from blokus_rl_amd.nets import build_model
+    from oracle.oracle import MCTSOracle, Oracle
+
+    o = Oracle(20, 4, 5)
+    torch.manual_seed(0)
+    model = build_model(model_type, 20, 4, o.A, num_res_blocks=5).cuda().eval() if model_type != "dumbnet" else None
+
+    def evaluate(s, player):
+        ids = o.legal_ids(s, player)
+        if model is None:
+            return ids, np.full(len(ids), 1.0 / len(ids), dtype=np.float32), np.zeros(4)
+        obs = torch.from_numpy(o.observe(s)).float().cuda().unsqueeze(0)
+        mask = torch.zeros(o.A, dtype=torch.bool, device="cuda")
+        mask[torch.from_numpy(ids).cuda()] = True
+        with torch.inference_mode():
+            lp, v = model(obs)
+            p = torch.exp(torch.log_softmax(torch.masked_select(lp[0], mask), dim=-1))
+        return ids, p.cpu().numpy(), v[0].cpu().numpy().astype(np.float64)
+
+    m = MCTSOracle(o, evaluate)
+    s = o.init_state()
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(100):
+            m.simulate(s)
+            n += 1
+        ids, pi = m.get_distribution(s, 0)
+        s, _ = o.next_state(s, int(ids[int(np.argmax(pi))]))
+        if o.game_ended(s) is not None:
+            s = o.init_state()
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "sims/s", "cores": 1, "kind": "port",
+            "sample": f"{n} simulations ({model_type} leaf eval{' on the GPU, batch 1' if model else ''}) "
+                      f"of one game from the empty board in {dt:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["legal", "selfplay"], default="legal")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["all", "legal", "selfplay"], default="all")
+    ap.add_argument("--legal-steps", type=int, default=200)
+    ap.add_argument("--legal-warmup", type=int, default=20)
     ap.add_argument("--boards", type=int, default=4096)
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--graph-steps", type=int, default=20)
@@ -200,9 +254,25 @@ def main():
     if args.workload == "legal":
         out = bench_legal(args, world, rank)
     else:
-        from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay
+        from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
-        out.pop("_selfplay", None)
+        if args.workload == "all":
+            # env + search alone: the uninformed-MCTS opponent (DumbNet, compare_arena.py:87-95)
+            _, _, dsims, dt, dctr, dms = run_selfplay("dumbnet", "fp32", args.games, args.sims, args.steps,
+                                                      args.warmup, rank, args.node_cap, world)
+            dsims_all = _sum_over_ranks(dsims, world)
+            out["uninformed_mcts"] = {"value": dsims_all / _max_over_ranks(dt, world), "unit": "sims/s",
+                                      "stage_ms_per_sim_step": dms, "engine_counters": dctr}
+            largs = argparse.Namespace(**vars(args))
+            largs.steps, largs.warmup, largs.no_cpu_baseline = args.legal_steps, args.legal_warmup, True
+            legal = bench_legal(largs, world, rank)
+            out["legal_move"] = {k: legal[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "roofline")}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_selfplay(args.cpu_seconds, args.model)
+            if args.workload == "all":
+                out["cpu_baseline_uninformed"] = cpu_baseline_selfplay(args.cpu_seconds / 2, "dumbnet")
+                out["legal_move"]["cpu_baseline"] = cpu_baseline_legal(legal["_states"], args.cpu_seconds / 2)
+    out.pop("_states", None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -88,7 +88,7 @@ class BatchedMCTS:
     def counters(self) -> dict:
         out = np.zeros(8, dtype=np.int64)
         _check(self.lib.bk_mcts_counters(self.h, out.ctypes.data_as(ctypes.c_void_p), self._s()))
-        keys = ["nodes", "children", "levels", "expanded", "terminal", "errors"]
+        keys = ["nodes", "children", "levels", "expanded", "terminal", "errors", "scanned", "leaf_children"]
         return {k: int(out[i]) for i, k in enumerate(keys)}
 
     def check(self):

@@ -62,13 +62,16 @@ class LeafEvaluator:
             self.const_v = torch.zeros((G, eng.P), dtype=torch.float32, device=dev)
             self.model = None
             return
-        self.model.eval()
-        self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32, device=dev)
+        from ..nets import inference_model
+        self.model = inference_model(model).to(memory_format=torch.channels_last)
+        self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32,
+                                      device=dev).contiguous(memory_format=torch.channels_last)
         self.graph = None
         if use_graph:
             self._capture()
 
     def _forward(self, obs):
+        obs = obs.contiguous(memory_format=torch.channels_last)
         with torch.inference_mode():
             if self.dtype != torch.float32:
                 with torch.autocast("cuda", dtype=self.dtype):

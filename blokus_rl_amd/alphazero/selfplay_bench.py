@@ -2,8 +2,8 @@
 
 Per GPU: 256 concurrent 4-player 20x20 games, 100 MCTS simulations per move, cpuct 1,
 temperature 1, first-ply Dirichlet(1) x 0.25, ResNet (5 blocks, 64 channels, A=30433,
-24.78M params) with random-init weights (seed 0) as the leaf evaluator in fp32. A step = one
-ply of every game (= 256 x 100 simulations). Ranks play independent games (seeded by rank).
+24.78M params) with random-init weights (seed 0) as the leaf evaluator. A step = one ply of
+every game (= 256 x 100 simulations). Ranks play independent games (seeded by rank).
 """
 from __future__ import annotations
 
@@ -16,46 +16,73 @@ from ..engine import Engine
 from ..nets import build_model
 from .selfplay import SelfPlay
 
-# Leaf-eval FLOPs of the default ResNet: 347.5 MFLOP per leaf.
-RESNET_FLOPS_PER_LEAF = 347.5e6
-FP32_PEAK = 157.3e12
+RESNET_FLOPS_PER_LEAF = 347.5e6  # SURVEY.md §3.2
+FP32_PEAK = 157.3e12             # MI355X_MICROARCH.md (f32 vector = f32 MFMA)
+FP16_PEAK = 2.5e15               # dense bf16/fp16 MFMA
+HBM_PEAK = 8.0e12
 
 
-def bench_selfplay(args, world, rank):
+def search_bytes(c: dict, sims: int, obs_bytes: int, mask_bytes: int) -> float:
+    """Algorithmic HBM bytes of the search kernels (k_select + k_expand_backup) from engine
+    counters: root state read per simulation; per descended level
+    16 B x K child stats + 52 B (hash probe, node header, child id, path record) + 40 B backup;
+    per expanded leaf the state, bitmask and observation row written, the bitmask re-read, 36 B
+    of node/value; per created child 4 B logit gather + 20 B child init."""
+    return (sims * 384 + c["scanned"] * 16 + c["levels"] * (52 + 40)
+            + c["expanded"] * (384 + mask_bytes + obs_bytes + mask_bytes + 36) + c["leaf_children"] * 24)
+
+
+def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, warmup: int, rank: int,
+                 node_cap: int, world: int, timers: bool = True):
     torch.manual_seed(0)
     eng = Engine(20, 4, 5)
-    G = args.games
-    model = build_model(args.model, 20, 4, eng.A, num_res_blocks=5).to(eng.device).eval()
-    nn_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.nn_dtype]
-    sp = SelfPlay(eng, model, G, num_sims=args.sims, seed=1234 + rank, nn_dtype=nn_dtype,
-                  node_cap=args.node_cap, continuous=True)
-    for _ in range(args.warmup):
+    model = build_model(model_type, 20, 4, eng.A, num_res_blocks=5).to(eng.device).eval()
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[nn_dtype]
+    sp = SelfPlay(eng, model, G, num_sims=sims, seed=1234 + rank, nn_dtype=dt, node_cap=node_cap, continuous=True)
+    for _ in range(warmup):
         sp.play_ply()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    c0 = sp.mcts.counters()
     sims0 = sp.stats.sims
-    sp.enable_timers(True)
+    if timers:
+        sp.enable_timers(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         sp.play_ply()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    sims = sp.stats.sims - sims0
+    c1 = sp.check_counters() if hasattr(sp, "check_counters") else sp.mcts.check()
+    done = sp.stats.sims - sims0
+    delta = {k: c1[k] - c0[k] for k in c1 if k not in ("errors", "nodes", "children")}
+    ms = sp.timer_ms() if timers else {}
+    return sp, eng, done, elapsed, delta, ms
+
+
+def bench_selfplay(args, world, rank):
+    G = args.games
+    sp, eng, sims, elapsed, delta, ms = run_selfplay(args.model, args.nn_dtype, G, args.sims, args.steps,
+                                                     args.warmup, rank, args.node_cap, world)
+    local_sims = sims
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        s = torch.tensor([sims], dtype=torch.float64, device="cuda")
-        dist.all_reduce(s)
-        sims = int(s.item())
-    ms = sp.timer_ms()
-    counters = sp.mcts.check()
-    return {
+        t = torch.tensor([elapsed, float(sims)], dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t)
+        elapsed, sims = float(tmax[0].item()), int(t[1].item())
+    steps_sim = args.steps * args.sims  # sim-steps timed (one simulation per tree each)
+    obs_bytes = 4 * 2 * eng.P * eng.N * eng.N
+    sbytes = search_bytes(delta, local_sims, obs_bytes, 8 * eng.W)
+    search_ms = ms.get("select", 0.0) + ms.get("expand", 0.0)
+    achieved = sbytes / steps_sim / (search_ms * 1e-3) if search_ms else 0.0
+    net_flops = RESNET_FLOPS_PER_LEAF * delta["expanded"] / steps_sim
+    net_peak = FP32_PEAK if args.nn_dtype == "fp32" else FP16_PEAK
+    out = {
         "metric": "MCTS sims/sec on 20x20 Blokus (4 players, 256 games/GPU, 100 sims/move)",
         "value": sims / elapsed,
         "unit": "sims/s",
@@ -67,11 +94,19 @@ def bench_selfplay(args, world, rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": f"{args.nn_dtype} net / f64 search / u32 bitboards",
-        "data": "synthetic: self-play from the empty board, random-init ResNet weights (seed 0)",
-        "config": {"workload": "config 3/4: AlphaZero self-play 20x20, 256 concurrent games per GPU, 100 sims/move",
-                   "global_batch": G * world, "parallelism": f"dp{world} (independent games)",
-                   "model": args.model},
+        "data": "synthetic: continuous self-play from the empty board, random-init ResNet weights (seed 0)",
+        "config": {"workload": "config 3 (N=1) / 4 (N=8): AlphaZero self-play 20x20, 256 concurrent games per GPU, "
+                               "100 sims/move, ResNet-5x64 leaf eval", "global_batch": G * world,
+                   "parallelism": f"dp{world} (independent games)", "model": args.model},
+        "roofline": {"bound": "hbm", "kernel": "k_select+k_expand_backup (search)",
+                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": None,
+                     "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms},
+        "net_roofline": {"bound": "mfma", "kernel": "ResNet forward (MIOpen/hipBLASLt, BN folded)",
+                         "achieved": net_flops / (ms.get("net", 1e9) * 1e-3) / 1e12 if ms else None,
+                         "peak": net_peak / 1e12, "unit": "TFLOP/s",
+                         "frac": (net_flops / (ms["net"] * 1e-3)) / net_peak if ms else None},
         "stage_ms_per_sim_step": ms,
-        "engine_counters": counters,
-        "_selfplay": sp,
+        "engine_counters": delta,
     }
+    return out

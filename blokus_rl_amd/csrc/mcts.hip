@@ -50,7 +50,7 @@ struct DevMcts {
   unsigned long long* counters;  // [8]
 };
 
-enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5 };
+enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5, kCtrScanned = 6, kCtrLeafK = 7 };
 enum { kErrChildPool = 1, kErrTable = 2, kErrDepth = 4, kErrIllegal = 8, kErrMissingRoot = 16 };
 
 __device__ __forceinline__ uint64_t table_key(const uint32_t* s) {
@@ -137,12 +137,15 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
   __syncthreads();
   double cp = cpuct;
   int depth = 0, err = 0;
+  long long scanned = 0;
   for (;;) {
     const int node = table_find(m, t, table_key(s), nullptr);
     if (node < 0) break;
     const size_t gn = (size_t)t * m.node_cap + node;
     const int64_t off = m.node_child[gn];
-    const int ci = select_child(m, off, m.node_K[gn], m.node_visits[gn], cp);
+    const int Kn = m.node_K[gn];
+    scanned += Kn;
+    const int ci = select_child(m, off, Kn, m.node_visits[gn], cp);
     const int a = m.ch_id[off + ci];
     if (depth >= kMaxDepth) { err |= kErrDepth; break; }
     if (apply_action(dp, s, a, fa)) { err |= kErrIllegal; break; }
@@ -195,6 +198,7 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
     status_out[t] = status;
     m.depth[t] = depth;
     atomicAdd(&m.counters[kCtrLevels], (unsigned long long)depth);
+    atomicAdd(&m.counters[kCtrScanned], (unsigned long long)scanned);
     if (status == 2) atomicAdd(&m.counters[kCtrTerminal], 1ull);
     if (err) atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
   }
@@ -272,6 +276,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
         m.tree_nodes[t] = node + 1;
         m.tree_children[t] = used + K;
         atomicAdd(&m.counters[kCtrExpanded], 1ull);
+        atomicAdd(&m.counters[kCtrLeafK], (unsigned long long)K);
       }
     } else if (l == 0) {
       atomicOr(&m.counters[kCtrErr], (unsigned long long)err);

@@ -107,3 +107,53 @@ def build_model(model_type: str, board_size: int, num_players: int, action_size:
         return DCNNet(board_size, num_players, action_size, kw.get("num_channels", 128), kw.get("linear_dim", 128),
                       kw.get("dropout", 0.3))
     return DumbNet(board_size, num_players, action_size)
+
+
+def _fold_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+    """conv followed by eval-mode BN -> one conv with scaled weights and shifted bias."""
+    fused = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding,
+                      bias=True).to(conv.weight.device)
+    with torch.no_grad():
+        scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        fused.weight.copy_(conv.weight * scale.view(-1, 1, 1, 1))
+        b = conv.bias if conv.bias is not None else torch.zeros_like(bn.running_mean)
+        fused.bias.copy_((b - bn.running_mean) * scale + bn.bias)
+    return fused
+
+
+class FusedResNet(nn.Module):
+    """Inference form of `ResNet` for the leaf batch: every eval-mode BatchNorm folded into its
+    convolution (MIOpen's inference BN costs as much as the convs at batch 256). Same function
+    as ResNet.eval() up to float32 rounding."""
+
+    def __init__(self, net: ResNet):
+        super().__init__()
+        net = net.eval()
+        self.stem = _fold_bn(net.conv1, net.bn1)
+        self.blocks = nn.ModuleList()
+        for blk in net.res_blocks:
+            self.blocks.append(nn.ModuleList([_fold_bn(blk[0], blk[1]), _fold_bn(blk[3], blk[4])]))
+        self.policy_conv = _fold_bn(net.policy_conv, net.policy_bn)
+        self.policy_out = net.policy_out
+        self.value_conv = _fold_bn(net.value_conv, net.value_bn)
+        self.value_fc1 = net.value_fc1
+        self.value_fc2 = net.value_fc2
+
+    def forward(self, x):
+        x = F.relu(self.stem(x))
+        h = x
+        for c1, c2 in self.blocks:
+            h = c2(F.relu(c1(h)))
+        x = F.relu(x + h)
+        p = F.relu(self.policy_conv(x)).flatten(1)
+        p = F.log_softmax(self.policy_out(p).float(), dim=1)
+        v = F.relu(self.value_conv(x)).flatten(1)
+        v = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v)))).float()
+        return p, v
+
+
+def inference_model(model: nn.Module) -> nn.Module:
+    """The leaf evaluator's form of a net (BN folded for ResNet, eval otherwise)."""
+    if isinstance(model, ResNet):
+        return FusedResNet(model).eval()
+    return model.eval()

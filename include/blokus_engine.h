@@ -164,7 +164,9 @@ int bk_mcts_leaf_info(bk_mcts* m, void* leaf_states, int32_t* depths, void* stre
 
 /* Engine counters (host copy, synchronises the stream): out[0] nodes used (all trees),
  * out[1] children used, out[2] selection levels descended (cumulative), out[3] leaves
- * expanded, out[4] terminal leaves, out[5] error flags (bit0 child pool full, bit1 table full). */
+ * expanded, out[4] terminal leaves, out[5] error flags (bit0 child pool full, bit1 table full,
+ * bit2 depth, bit3 illegal child, bit4 root missing), out[6] children scanned by selection
+ * (sum of K over descended nodes), out[7] children created by expansion. */
 int bk_mcts_counters(bk_mcts* m, int64_t* out, void* stream);
 
 #ifdef __cplusplus
