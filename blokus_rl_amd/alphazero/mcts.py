@@ -1,0 +1,69 @@
+"""Drop-in `MCTS` (blokus_rl/alphazero/mcts.py:7-99) on the GPU search engine.
+
+`MCTS(game, nn)`, `.simulate(s, current_player, cpuct=1, epsilon_fix=True) -> scores` and
+`.get_distribution(s, temperature) -> object array (K, 2) of [array([id]), prob]` behave as the
+reference's (same selection rule, backup, tie-breaking, float64 statistics): the tree is a
+one-tree BatchedMCTS. `nn` may be this package's BlokusNNetWrapper (device path: log-probs over
+all ids, masked softmax inside k_expand_backup) or any object with the reference's
+`predict(obs, mask) -> (p over legal ids, v)` (its p is handed to the engine as is).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .batched_mcts import BatchedMCTS
+
+
+class MCTS:
+    def __init__(self, game, nn, node_cap: int = 16384, child_cap: int | None = None):
+        self.game = game
+        self.nn = nn
+        eng = game.engine
+        self._eng = eng
+        self._m = BatchedMCTS(eng, 1, node_cap=node_cap, child_cap=child_cap or node_cap * (256 if eng.N >= 14 else 64))
+        self._logp = torch.zeros((1, eng.A), dtype=torch.float32, device=eng.device)
+        self._vals = torch.zeros((1, eng.P), dtype=torch.float32, device=eng.device)
+
+    @property
+    def tree(self):
+        """Size view of the transposition table (the reference exposes its dict)."""
+        return {"nodes": self._m.counters()["nodes"]}
+
+    def simulate(self, s, current_player: int, cpuct: float = 1, epsilon_fix: bool = True):
+        if not epsilon_fix:
+            raise NotImplementedError("the engine always uses sqrt(sum N + 1e-6) (epsilon_fix=True)")
+        roots = self.game._dev(s)
+        status, obs, mask = self._m.select(roots, None, float(cpuct))
+        st = int(status[0])
+        if st == 2:
+            leaves, _ = self._m.leaf_info()
+            _, scores = self._eng.game_ended(leaves)
+            self._m.expand_backup(self._logp, self._vals, prior_mode=1)
+            return scores[0].cpu().numpy()
+        if st != 1:
+            self._m.check()
+            raise RuntimeError("MCTS select failed")
+        if hasattr(self.nn, "predict_batch"):
+            logp, v = self.nn.predict_batch(obs)
+            self._m.expand_backup(logp, v, prior_mode=0)
+            return v[0].cpu().numpy()
+        mask_f = self._eng.unpack_mask(mask)[0].cpu().numpy().astype(np.float64)
+        p, v = self.nn.predict(obs[0].cpu().numpy(), mask_f)
+        ids = torch.from_numpy(np.nonzero(mask_f)[0]).to(self._eng.device)
+        self._logp.zero_()
+        self._logp[0, ids] = torch.as_tensor(np.atleast_1d(p), dtype=torch.float32, device=self._eng.device)
+        self._vals[0] = torch.as_tensor(np.asarray(v, dtype=np.float32), device=self._eng.device)
+        self._m.expand_backup(self._logp, self._vals, prior_mode=1)
+        return v
+
+    def get_distribution(self, s, temperature):
+        roots = self.game._dev(s)
+        ids, pi, counts = self._m.root_policy(roots, None, float(temperature))
+        K = int(counts[0])
+        if K < 0:
+            raise KeyError(self.game.string_representation(s))
+        out = np.zeros((K, 2), dtype=np.object_)
+        out[:, 0] = [np.array([i]) for i in ids[0, :K].cpu().tolist()]
+        out[:, 1] = pi[0, :K].cpu().numpy()
+        return out

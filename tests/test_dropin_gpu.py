@@ -1,0 +1,177 @@
+"""The drop-in boundary classes on the GPU engine, read like the reference's own call sites:
+ColosseumBlokusGameWrapper (blokus_wrapper.py), MCTS (mcts.py) driven exactly as
+trainer._self_play / MCTSPlayer drive it, BlokusNNetWrapper.predict / predict_batch, the
+arena and the Coach's self-play."""
+import importlib.util
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from mcts_golden_util import load_cases, prior_value, state_of, unhex
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _hp(**kw):
+    from blokus_rl_amd.hparams import AlphaZeroHparams
+    return AlphaZeroHparams(**kw)
+
+
+@pytest.fixture(scope="module")
+def game20():
+    from blokus_rl_amd.colossumrl import ColosseumBlokusGameWrapper
+    return ColosseumBlokusGameWrapper(_hp(board_size=20, number_of_players=4))
+
+
+@pytest.fixture(scope="module")
+def game7():
+    from blokus_rl_amd.colossumrl import ColosseumBlokusGameWrapper
+    return ColosseumBlokusGameWrapper(_hp(board_size=7, number_of_players=2))
+
+
+def test_game_wrapper_matches_oracle(game20):
+    o = Oracle(20, 4, 5)
+    g = game20
+    assert g.get_action_size() == 30433 and g.get_observation_size() == [8, 20, 20]
+    s, p = g.get_init_board()
+    assert p == 0 and (s == o.init_state()).all()
+    rng = np.random.default_rng(0)
+    while g.get_game_ended(s) is None:
+        mask = g.get_valid_moves(s, p)
+        assert mask.dtype == np.float64 and mask.shape == (30433,)
+        ids = np.nonzero(mask)[0]
+        assert (ids == o.legal_ids(s)).all()
+        other = (p + 1) % 4
+        assert (np.nonzero(g.get_valid_moves(s, other))[0] == o.legal_ids(s, other)).all()
+        obs, m2 = g.get_observation(s, p)
+        assert (obs == o.observe(s)).all() and (m2 == mask).all()
+        assert g.string_representation(s) == o.hash(s)
+        a = int(rng.choice(ids))
+        s2, p2 = g.get_next_state(s, p, a)
+        ref, refp = o.next_state(s, a)
+        assert (s2 == ref).all() and p2 == refp
+        # strings round-trip through the action dicts (blokus_wrapper.py:102)
+        s3, _ = g.get_next_state(s, p, g.action_move_dict[a])
+        assert (s3 == s2).all()
+        s, p = s2, p2
+    assert (g.get_game_ended(s) == o.game_ended(s)).all()
+    with pytest.raises(KeyError):
+        g.get_next_state(s, p, "no-such-move")
+
+
+def test_illegal_id_raises(game20):
+    s, p = game20.get_init_board()
+    with pytest.raises(ValueError):
+        game20.get_next_state(s, p, 5)
+
+
+class _StubNet:
+    """Reference-style predict(obs, mask) -> (p, v) from the golden prior function."""
+
+    def __init__(self, game, o):
+        self.game, self.o = game, o
+        self.last = None
+
+    def predict(self, obs, mask):
+        ids = np.nonzero(mask)[0]
+        # recover the leaf state's hash: the engine's obs rows + mask are not enough, so the
+        # stub keeps a board->hash map filled through the game wrapper's observation
+        h = self.o.hash(self._state_from_obs(obs))
+        p, v = prior_value(h, len(ids), self.o.P)
+        return p, v
+
+    def _state_from_obs(self, obs):
+        P, N = self.o.P, self.o.N
+        cells = np.zeros((N, N), dtype=np.int8)
+        for k in range(P):
+            cells[obs[k] > 0.5] = k + 1
+        tm = int(np.argmax([obs[P + k, 0, 0] for k in range(P)]))
+        # hash is board-only: pieces / to_move / flags do not enter it
+        return self.o.make_state(cells, [0, 0, 0, 0], tm)
+
+
+@pytest.mark.parametrize("k", [0, 3, 6])
+def test_dropin_mcts_matches_reference(k, game20, game7):
+    """MCTS.simulate / get_distribution called the way trainer._self_play calls them, with the
+    reference-style predict() stub; distributions and root visit counts equal the golden
+    vectors of the reference mcts.py."""
+    from blokus_rl_amd.alphazero.mcts import MCTS
+    from blokus_rl_amd.colossumrl import ColosseumBlokusGameWrapper
+
+    case = load_cases()[k]
+    preset = tuple(case["preset"])
+    g = {(20, 4, 5): game20, (7, 2, 5): game7}.get(preset) or ColosseumBlokusGameWrapper(
+        _hp(board_size=preset[0], number_of_players=preset[1], max_piece_cells=preset[2]))
+    o = Oracle(*preset)
+    tree = MCTS(g, _StubNet(g, o), node_cap=4096)
+    for mv in case["moves"]:
+        s = state_of(mv["root"])
+        p = g.to_move(s)
+        for _ in range(mv["sims"]):
+            tree.simulate(s, p, cpuct=case["cpuct"])
+        d1 = tree.get_distribution(s, 1)
+        d0 = tree.get_distribution(s, 0)
+        assert [int(x[0]) for x in d1[:, 0]] == mv["ids"]
+        assert list(d1[:, 1]) == unhex(mv["dist_T1"])
+        assert list(d0[:, 1]) == unhex(mv["dist_T0"])
+
+
+def test_predict_batch_matches_reference_predict(game20):
+    """The device leaf path (BN-folded net, masked softmax in k_expand_backup) against the
+    reference predict() golden rows, float32 tolerance."""
+    from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
+    from blokus_rl_amd.neural_network import BlokusNNetWrapper
+
+    spec = importlib.util.spec_from_file_location("mng", os.path.join(GOLDEN, "make_net_golden.py"))
+    mng = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mng)
+    G = np.load(os.path.join(GOLDEN, "net_golden.npz"))
+    nn = BlokusNNetWrapper(game20, _hp(num_res_blocks=2), device=game20.device)
+    sd = nn.model.state_dict()
+    nn.model.load_state_dict({k: v.to(game20.device) for k, v in mng.det_state_dict({k: v.shape for k, v in sd.items()}).items()})
+    for i in range(3):
+        obs = torch.from_numpy(G[f"obs20_{i}"]).unsqueeze(0).to(game20.device)
+        lp, v = nn.predict_batch(obs)
+        ids = torch.from_numpy(G[f"ids20_{i}"]).long().to(game20.device)
+        p = torch.softmax(lp[0, ids], dim=0).cpu().numpy()
+        np.testing.assert_allclose(p, G[f"p20_{i}"], rtol=2e-3, atol=1e-6)
+        np.testing.assert_allclose(v[0].cpu().numpy(), G[f"v20_{i}"], atol=1e-4)
+        pr, vr = nn.predict(G[f"obs20_{i}"], np.isin(np.arange(30433), G[f"ids20_{i}"]).astype(np.float64))
+        np.testing.assert_allclose(pr, G[f"p20_{i}"], rtol=2e-3, atol=1e-6)
+
+
+def test_arena_and_players_7x7(game7):
+    from blokus_rl_amd.alphazero.arena import play_match
+    from blokus_rl_amd.neural_network import BlokusNNetWrapper
+    from blokus_rl_amd.players import MCTSPlayer, RandomPlayer
+
+    np.random.seed(0)
+    nn = BlokusNNetWrapper(game7, _hp(board_size=7, number_of_players=2, model_type="dumbnet"), device=game7.device)
+    players = [MCTSPlayer(game7, nn, 20), RandomPlayer(game7)]
+    scores, items = play_match(game7, players, games_num=2, permute=True)
+    assert scores.shape == (2,) and len(items) == 2
+    for it in items:
+        assert sorted(it["scores"].tolist()) in ([-1.0, 3.0], [1.0, 1.0])
+
+
+def test_coach_self_play_7x7():
+    from blokus_rl_amd.alphazero.trainer import AlphaZeroTrainer
+
+    np.random.seed(42)
+    hp = _hp(board_size=7, number_of_players=2, model_type="resnet", num_res_blocks=1, num_mcts_sims=8,
+             games_per_gpu=4, num_eps=4, epochs=1, batch_size=16, checkpoint_dir="/tmp/bkaz/ck", data_dir="/tmp/bkaz/data")
+    tr = AlphaZeroTrainer(hp)
+    data = tr._self_play(1.0)  # the reference episode, one game, np.random driven
+    assert len(data) > 0 and all(d[3] is not None for d in data)
+    for obs, mask, pi, z in data:
+        assert obs.shape == (4, 7, 7) and mask.shape == (2522,)
+        assert abs(float(pi.sum()) - 1.0) < 1e-4 and len(pi) == int(mask.sum())
+    batched = tr.self_play_batched(4)
+    assert len(batched) > 0
+    loss = tr._train_epochs(batched)
+    assert np.isfinite(loss)
