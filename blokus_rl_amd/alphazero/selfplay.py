@@ -131,6 +131,7 @@ class SelfPlay:
         self._pending: list[tuple[torch.Tensor, ...]] = []  # per-ply records awaiting z
         self.timers = None
         self.finished: list[Examples] = []
+        self._window: list[tuple[torch.Tensor, ...]] = []  # records since mark_window()
 
     # ------------------------------------------------------------------ one simulation
     def simulate(self):
@@ -188,8 +189,10 @@ class SelfPlay:
         action = torch.where(act_mask, action, torch.full_like(action, -1)).to(torch.int32).contiguous()
         if record:
             player = Engine.to_move(self.roots).clone()
-            self._pending.append((self.roots.clone(), ids.to(torch.int16), pi32, counts.clone(), player,
-                                  self.game_id.clone(), act_mask.clone()))
+            rec = (self.roots.clone(), ids.to(torch.int16), pi32, counts.clone(), player, self.game_id.clone(),
+                   act_mask.clone())
+            self._pending.append(rec)
+            self._window.append(rec)
         self.roots, _, status = self.eng.next_state(self.roots, action)
         self.first_ply &= ~act_mask
         self.stats.plies += 1
@@ -229,6 +232,27 @@ class SelfPlay:
             self.next_game_id += n
         else:
             self.active = self.active & ~flags
+
+    def mark_window(self):
+        self._window = []
+
+    def window_packed(self):
+        """Packed replay rows (blokus_rl_amd.replay layout) of every ply recorded since
+        mark_window(); z is zero for games still running (their outcome is not known yet)."""
+        from ..replay import pack
+
+        if not self._window:
+            return None, 0
+        m = torch.cat([r[6] for r in self._window])
+        states = torch.cat([r[0] for r in self._window])[m]
+        k = torch.cat([r[3] for r in self._window])[m]
+        kmax = int(k.max().item())
+        cap = max(64, (kmax + 63) // 64 * 64)
+        ids = torch.cat([r[1][:, :cap] for r in self._window])[m]
+        pi = torch.cat([r[2][:, :cap] for r in self._window])[m]
+        player = torch.cat([r[4] for r in self._window])[m]
+        z = torch.zeros((states.shape[0], self.eng.P), dtype=torch.float32, device=self.eng.device)
+        return pack(states, ids, pi, k, z, player, cap=cap)
 
     def run(self, plies: int):
         t0 = time.perf_counter()

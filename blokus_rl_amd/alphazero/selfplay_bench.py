@@ -49,9 +49,21 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     sims0 = sp.stats.sims
     if timers:
         sp.enable_timers(True)
+    sp.mark_window()
+    gather = {}
     t0 = time.perf_counter()
     for _ in range(steps):
         sp.play_ply()
+    if world > 1:
+        # config 4: the (s, pi, z) rows of the timed plies, all-gathered over RCCL/xGMI
+        from ..replay import all_gather_packed
+
+        tg = time.perf_counter()
+        buf, cap = sp.window_packed()
+        rows, _ = all_gather_packed(buf, cap)
+        torch.cuda.synchronize()
+        gather = {"rows_sent": int(buf.shape[0]), "rows_received": int(rows.shape[0]),
+                  "bytes_received": int(rows.numel()), "seconds": time.perf_counter() - tg}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -61,6 +73,8 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     done = sp.stats.sims - sims0
     delta = {k: c1[k] - c0[k] for k in c1 if k not in ("errors", "nodes", "children")}
     ms = sp.timer_ms() if timers else {}
+    if gather:
+        ms["all_gather"] = gather
     return sp, eng, done, elapsed, delta, ms
 
 

@@ -1,0 +1,69 @@
+"""The N>1 path on CPU: two gloo ranks exchange packed replay examples (ragged row counts and
+different caps) with all_gather_packed; every rank must receive every row bit-exactly."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _examples(rank: int):
+    g = torch.Generator().manual_seed(100 + rank)
+    E = 5 + 3 * rank
+    K = 70 + 100 * rank
+    states = torch.randint(0, 256, (E, 384), dtype=torch.uint8, generator=g)
+    k = torch.randint(1, K + 1, (E,), generator=g).to(torch.int32)
+    ids = torch.randint(0, 30433, (E, K), generator=g).to(torch.int16)
+    pi = torch.rand((E, K), generator=g)
+    col = torch.arange(K).unsqueeze(0)
+    ids = torch.where(col < k.unsqueeze(1), ids, torch.full_like(ids, -1))
+    pi = torch.where(col < k.unsqueeze(1), pi, torch.zeros_like(pi))
+    z = torch.tensor([[3.0, -1.0, -1.0, -1.0]]).repeat(E, 1)
+    player = torch.arange(E, dtype=torch.int32) % 4
+    return states, ids, pi, k, z, player
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from blokus_rl_amd.replay import all_gather_packed, pack, unpack
+    buf, cap = pack(*_examples(rank)[:5], player=_examples(rank)[5])
+    rows, cmax = all_gather_packed(buf, cap)
+    u = unpack(rows, cmax)
+    ok = True
+    off = 0
+    for r in range(world):
+        states, ids, pi, k, z, player = _examples(r)
+        E, K = ids.shape
+        sl = slice(off, off + E)
+        ok &= torch.equal(u["states"][sl], states) and torch.equal(u["k"][sl], k)
+        ok &= torch.equal(u["player"][sl], player) and torch.equal(u["z"][sl], z)
+        ok &= torch.equal(u["ids"][sl, :K], ids) and torch.equal(u["pi"][sl, :K], pi)
+        ok &= bool((u["ids"][sl, K:] == -1).all())
+        off += E
+    ok &= off == rows.shape[0]
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_all_gather_packed_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
