@@ -3,8 +3,11 @@
 #include <cstring>
 #include <string>
 
+#include <cstdlib>
+
 #include "../../include/blokus_engine.h"
 #include "ctx.h"
+#include "legal_rows.h"
 
 namespace bk {
 
@@ -166,12 +169,31 @@ int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int devi
   const Preset& p = c->pre;
   DevPreset& d = c->dp;
   d.N = p.N; d.P = p.P; d.A = p.A; d.W64 = p.mask_words; d.W32 = p.mask_words32;
-  d.W32pad = 2 * p.mask_words;
+  d.W32pad = 4 * ((p.mask_words + 1) / 2);  // 16-B aligned rows of u32 in LDS
   d.num_items = p.num_items; d.num_pieces = p.num_pieces;
   d.full_pieces = p.full_pieces;
   d.full_row = (1u << p.N) - 1u;
   for (int k = 0; k < kMaxP; ++k) { d.corner_r[k] = (int8_t)p.corner_r[k]; d.corner_c[k] = (int8_t)p.corner_c[k]; }
   for (int i = 0; i <= kNumPieces; ++i) d.piece_item_off[i] = (int16_t)p.piece_item_off[i];
+  // the unrolled kernel's compile-time orientations must be the host tables' orientations
+  bool same = (int)p.orients.size() <= kNumOrient;
+  for (size_t o = 0; same && o < p.orients.size(); ++o) {
+    const std::vector<int>& od = p.orients[o];
+    const OrientC& k = kOrient[o];
+    same = od[0] == k.piece && od[1] == k.h && od[2] == k.w && od[3] == k.n;
+    for (int q = 0; same && q < 5; ++q) same = od[4 + q] == k.dr[q] && od[9 + q] == k.dc[q];
+  }
+  if (!same) {
+    delete c;
+    set_error("orient_table.h disagrees with the host orientation tables (re-run gen_orient.py)");
+    return BK_EINVAL;
+  }
+  {
+    const char* e = std::getenv("BK_LEGAL_KERNEL");
+    c->legal_items_kernel = e && std::string(e) == "items";
+    const char* w = std::getenv("BK_LEGAL_WPB");  // waves per workgroup (A/B knob)
+    c->legal_wpb = w ? std::atoi(w) : 11;
+  }
   if (device < 0) {  // host-only context: tables, no device memory (CPU tests, tooling)
     *out = c;
     return BK_OK;
@@ -230,9 +252,36 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
   BK_REQUIRE(c && states && mask_words && B >= 0, "bad argument");
   BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
   if (B == 0) return BK_OK;
-  hipLaunchKernelGGL(k_legal_mask, dim3(B), dim3(kWave), mask_lds_bytes(c->dp), (hipStream_t)stream, c->dp,
-                     (const uint32_t*)states, players, B, mask_words, counts);
-  return launch_check("k_legal_mask");
+  if (c->legal_items_kernel) {  // A/B reference: the item-loop kernel (BK_LEGAL_KERNEL=items)
+    hipLaunchKernelGGL(k_legal_mask, dim3(B), dim3(kWave), mask_lds_bytes(c->dp), (hipStream_t)stream, c->dp,
+                       (const uint32_t*)states, players, B, mask_words, counts);
+    return launch_check("k_legal_mask");
+  }
+  const int bpw = kWave / c->dp.N;
+  const size_t lds = sizeof(uint32_t) * (size_t)bpw * (size_t)c->dp.W32pad;
+  const dim3 grid((B + bpw - 1) / bpw);
+  const hipStream_t st = (hipStream_t)stream;
+  const uint32_t* sp = (const uint32_t*)states;
+#define BK_LEGAL_LAUNCH(W, S) \
+  hipLaunchKernelGGL((k_legal_mask_rows<W, S>), grid, dim3(64 * W), lds, st, c->dp, sp, players, B, mask_words, counts)
+  switch (c->legal_wpb) {
+    case 1: BK_LEGAL_LAUNCH(1, 0); break;
+    case 2: BK_LEGAL_LAUNCH(2, 0); break;
+    case 4: BK_LEGAL_LAUNCH(4, 0); break;
+    case 12: BK_LEGAL_LAUNCH(2, 1); break;
+    case 14: BK_LEGAL_LAUNCH(4, 1); break;
+    case 21:  // two boards per wave (balanced grid at B = 4096)
+      if (c->dp.N * 2 <= kWave) {
+        hipLaunchKernelGGL((k_legal_mask_rows<1, 0, 2>), dim3((B + 1) / 2), dim3(64),
+                           sizeof(uint32_t) * 2 * (size_t)c->dp.W32pad, st, c->dp, sp, players, B, mask_words, counts);
+        break;
+      }
+      BK_LEGAL_LAUNCH(1, 0);
+      break;
+    default: BK_LEGAL_LAUNCH(1, 1); break;  // 11: one wave per group, even/odd split
+  }
+#undef BK_LEGAL_LAUNCH
+  return launch_check("k_legal_mask_rows");
 }
 
 int bk_legal_ids(bk_ctx* c, const void* states, const int32_t* players, int B, int32_t* ids, int cap,

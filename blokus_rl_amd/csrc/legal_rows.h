@@ -1,0 +1,182 @@
+// legal_rows.h — the batched legal-move bitmask kernel (bk_legal_mask), row-parallel form.
+//
+// Mapping: one 64-lane wave holds floor(64/N) boards, one lane per board row (N=20 -> 3 boards,
+// lanes 0-59; N=7 -> 9 boards). Each lane keeps its row and the next four rows of the mover's
+// forbidden / anchor bitboards BIT-REVERSED in registers, so "cell (dr, dc) of a placement with
+// origin column c" is bit (31-c) of rev_row[dr] << dc: one v_lshl_or_b32 per cell and plane.
+// The 91 fixed orientations are unrolled at compile time from orient_table.h, so the inner
+// loop has no table loads and every cell offset is an immediate. For each orientation the lane
+// produces the W legal origin columns of its origin row and ORs that W-bit field into its
+// board's LDS bitmask at bit base_o + r*W; the masks then stream out as u64 rows.
+#pragma once
+#include <utility>
+
+#include "common.h"
+#include "orient_table.h"
+
+namespace bk {
+
+struct RowCtx {
+  uint32_t fr[5];      // bit-reversed forbidden rows r..r+4
+  uint32_t ar[5];      // bit-reversed anchor rows r..r+4
+  uint32_t rowok[6];   // rowok[h] = ~0 when a placement of height h fits below row r (and the lane is real)
+  uint32_t pieces;     // unused pieces of the mover
+  int rN1;             // r * (N + 1): bit offset of origin row r is base + r*(N+1) - r*w
+  int r;
+  uint32_t* mb;        // this lane's board bitmask in LDS
+};
+
+// One fixed orientation for one origin row, branch-free: 2 ops per cell (v_lshl_or into the
+// forbidden and anchor accumulators), then legal = anchor & ~forbidden, validity masks, and the
+// W-bit field ORed into the board's LDS bitmask (two 32-bit ORs; the second is 0 unless the field
+// straddles a word).
+template <int O, int WPB, int SPLIT>
+__device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c, int wave, int& base) {
+  constexpr OrientC oc = kOrient[O];
+  if (oc.piece >= dp.num_pieces) return;  // wave-uniform (presets use a prefix of the pieces)
+  const int W = dp.N - oc.w + 1;
+  const int R = dp.N - oc.h + 1;
+  if (WPB > 1 && (O % WPB) != wave) {  // another wave of the workgroup owns this orientation
+    base += R * W;
+    return;
+  }
+  uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
+  uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
+#pragma unroll
+  for (int k = 1; k < oc.n; ++k) {
+    bad |= c.fr[oc.dr[k]] << oc.dc[k];
+    good |= c.ar[oc.dr[k]] << oc.dc[k];
+  }
+  const uint32_t colmask = (1u << W) - 1u;  // wave-uniform
+  const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
+  const uint32_t v = __brev(good & ~bad) & colmask & c.rowok[oc.h] & pmask;
+  const int bit = base + c.rN1 - c.r * oc.w;
+  const uint64_t x = (uint64_t)v << (bit & 31);
+  uint32_t* dst = c.mb + (bit >> 5);
+  if (SPLIT) {
+    // even and odd origin rows in separate LDS instructions: two lanes of one instruction are
+    // >= 2W >= 32 bits apart, so they never OR into the same word (no same-address serialisation)
+    if ((c.r & 1) == 0) {
+      atomicOr(dst, (uint32_t)x);
+      atomicOr(dst + 1, (uint32_t)(x >> 32));
+    }
+    if (c.r & 1) {
+      atomicOr(dst, (uint32_t)x);
+      atomicOr(dst + 1, (uint32_t)(x >> 32));
+    }
+  } else {
+    atomicOr(dst, (uint32_t)x);
+    atomicOr(dst + 1, (uint32_t)(x >> 32));
+  }
+  base += R * W;
+}
+
+template <int WPB, int SPLIT, size_t... Os>
+__device__ __forceinline__ void orient_all(const DevPreset& dp, const RowCtx& c, int wave,
+                                           std::index_sequence<Os...>) {
+  int base = 0;
+  (orient_step<(int)Os, WPB, SPLIT>(dp, c, wave, base), ...);
+}
+
+// Workgroup = WPB waves sharing one group of boards_per_wave boards: wave w evaluates the
+// orientations O with O % WPB == w (round robin keeps the cell work balanced), all OR into the
+// same LDS masks, then the WPB waves stream the masks out together.
+// LDS: boards_per_wave * W32pad words. Grid: ceil(B / boards_per_wave) blocks of 64*WPB.
+template <int WPB, int SPLIT, int BPW = 0>
+__global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, const uint32_t* __restrict__ states,
+                                                              const int32_t* __restrict__ players, int B,
+                                                              uint64_t* __restrict__ masks,
+                                                              int32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t m32[];
+  __shared__ int cnt_sh[kWave];
+  const int l = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int N = dp.N;
+  const int bpw = BPW ? BPW : kWave / N;
+  const int j = l / N;
+  const int r = l - j * N;
+  const int b0 = blockIdx.x * bpw;
+  const int b = b0 + j;
+  const bool ok = j < bpw && b < B;
+  for (int i = threadIdx.x; i < bpw * dp.W32pad / 4; i += kWave * WPB)
+    reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (threadIdx.x < kWave) cnt_sh[threadIdx.x] = 0;
+
+  uint32_t o0 = 0u, o1 = 0u, o2 = 0u, o3 = 0u, pieces4[kMaxP] = {0u, 0u, 0u, 0u};
+  int q = 0;
+  if (ok) {  // independent loads: the four colour rows, the four piece sets, the mover
+    const uint32_t* s = states + (size_t)b * kStateWords;
+    o0 = s[r];
+    o1 = s[kMaxN + r];
+    o2 = s[2 * kMaxN + r];
+    o3 = s[3 * kMaxN + r];
+#pragma unroll
+    for (int k = 0; k < kMaxP; ++k) pieces4[k] = s[kWPieces + k];
+    q = players ? players[b] : -1;
+    if (q < 0) q = (int)s[kWToMove];
+  }
+  const uint32_t own = q == 0 ? o0 : q == 1 ? o1 : q == 2 ? o2 : o3;
+  const uint32_t pieces = q == 0 ? pieces4[0] : q == 1 ? pieces4[1] : q == 2 ? pieces4[2] : pieces4[3];
+  const uint32_t occ = o0 | o1 | o2 | o3;
+  const uint32_t up_raw = __shfl(own, l - 1 < 0 ? 0 : l - 1, kWave);
+  const uint32_t dn_raw = __shfl(own, l + 1 > kWave - 1 ? kWave - 1 : l + 1, kWave);
+  const uint32_t up = r > 0 ? up_raw : 0u;
+  const uint32_t dn = r + 1 < N ? dn_raw : 0u;
+  const uint64_t owners = __ballot(ok && own != 0u);
+  const uint64_t rows_of_board = (N >= 64 ? ~0ull : ((1ull << N) - 1ull)) << (j * N);
+  const bool first = (owners & rows_of_board) == 0ull;
+  uint32_t forb = 0u, anch = 0u;
+  if (ok) {
+    forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
+    if (first)
+      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+    else
+      anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
+  }
+  RowCtx c;
+  c.fr[0] = __brev(forb);
+  c.ar[0] = __brev(anch);
+#pragma unroll
+  for (int d = 1; d < 5; ++d) {
+    const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
+    c.fr[d] = __shfl(c.fr[0], src, kWave);
+    c.ar[d] = __shfl(c.ar[0], src, kWave);
+  }
+  c.r = r;
+  c.rN1 = r * (N + 1);
+  c.pieces = pieces;
+#pragma unroll
+  for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
+  c.mb = m32 + (j < bpw ? j : 0) * dp.W32pad;
+  __syncthreads();  // mask zeroing complete
+  orient_all<WPB, SPLIT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+  __syncthreads();
+  // stream out every board of the group: 16-B stores when rows are 16-B aligned (W64 even);
+  // popcounts accumulate per lane, one wave reduction and one LDS add per board
+  const int nb = B - b0 < bpw ? B - b0 : bpw;
+  for (int jj = 0; jj < nb; ++jj) {
+    int cnt = 0;
+    if ((dp.W64 & 1) == 0) {
+      const uint4* src = reinterpret_cast<const uint4*>(m32 + jj * dp.W32pad);
+      uint4* dst = reinterpret_cast<uint4*>(masks + (size_t)(b0 + jj) * dp.W64);
+      for (int p = threadIdx.x; p < dp.W64 / 2; p += kWave * WPB) {
+        const uint4 v = src[p];
+        dst[p] = v;
+        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+      }
+    } else {
+      for (int p = threadIdx.x; p < dp.W64; p += kWave * WPB) {
+        const uint32_t* src = m32 + jj * dp.W32pad + 2 * p;
+        const uint64_t v = (uint64_t)src[0] | ((uint64_t)src[1] << 32);
+        masks[(size_t)(b0 + jj) * dp.W64 + p] = v;
+        cnt += __popcll(v);
+      }
+    }
+    cnt = wave_sum(cnt);
+    if (l == 0) atomicAdd(&cnt_sh[jj], cnt);
+  }
+  __syncthreads();
+  if (counts && threadIdx.x < nb) counts[b0 + threadIdx.x] = cnt_sh[threadIdx.x];
+}
+
+}  // namespace bk

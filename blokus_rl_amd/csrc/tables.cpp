@@ -116,6 +116,12 @@ bool build_preset(int N, int P, int max_cells, Preset* pr) {
           if (dc[n] + 1 > w) w = dc[n] + 1;
           ++n;
         }
+      {
+        std::vector<int> od = {pc, h, w, n};
+        for (int q = 0; q < 5; ++q) od.push_back(q < n ? dr[q] : dr[0]);
+        for (int q = 0; q < 5; ++q) od.push_back(q < n ? dc[q] : dc[0]);
+        p.orients.push_back(od);
+      }
       const int R = N - h + 1, W = N - w + 1;
       for (int r = 0; r < R; ++r) {
         const int item = p.num_items++;

@@ -57,6 +57,8 @@ struct Preset {
   int corner_r[kMaxP] = {0}, corner_c[kMaxP] = {0};
   int piece_item_off[kNumPieces + 1] = {0};  // items of piece i: [off[i], off[i+1])
   std::vector<uint64_t> items;     // [num_items]
+  // per fixed orientation (canonical order): piece, h, w, n, dr[5], dc[5] (unused cells = cell 0)
+  std::vector<std::vector<int>> orients;
   std::vector<uint32_t> act;       // [A]: item index (low 16) | origin col << 16 | piece << 24
   std::vector<int32_t> act_table;  // [A*4]: piece, orientation, row, col
   std::vector<int16_t> act_cells;  // [A*5]: r*N + c, -1 pad
