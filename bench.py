@@ -188,6 +188,77 @@ def cpu_baseline_legal(states: torch.Tensor, seconds: float):
             "sample": f"{n} board evaluations (first 256 benchmark boards, repeated) in {dt:.1f} s"}
 
 
+# Config 5 algorithmic bytes per env-step: state read + write (768), action (4), rng (16),
+# obs (49 u8), mask (15 u64 = 120 at 919 ids), reward + done (8). DESIGN.md §4.
+VEC_BYTES_PER_STEP = 768 + 4 + 16 + 49 + 120 + 8
+
+
+def bench_vecenv(args, world, rank):
+    """Config 5: the PPO 7x7 vector env, E envs, one fused k_vec_step launch per vector step."""
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    E = args.envs
+    env = BlokusVectorEnv(E, 7, 4)
+    env.reset(seed=rank)
+    stream = torch.cuda.current_stream()
+    for _ in range(20):
+        env.step(None)
+    torch.cuda.synchronize()
+    _barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.vec_steps):
+        env.step(None)  # in-kernel random agent (policy stand-in), then the random opponent
+    e1.record(stream)
+    torch.cuda.synchronize()
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    kernel_ms = e0.elapsed_time(e1) / args.vec_steps
+    # PPO-style: the agent's actions sampled on the device from masked logits each step
+    logits = torch.zeros((E, env.eng.A), device=env.device)
+    for _ in range(5):
+        a = torch.distributions.Categorical(logits=env.masked_logits(logits)).sample()
+        env.step(a)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    n2 = max(10, args.vec_steps // 10)
+    for _ in range(n2):
+        a = torch.distributions.Categorical(logits=env.masked_logits(logits)).sample()
+        env.step(a)
+    torch.cuda.synchronize()
+    dt2 = time.perf_counter() - t1
+    achieved = VEC_BYTES_PER_STEP * E / (kernel_ms * 1e-3)
+    out = {"metric": "PPO vector-env steps/sec (7x7, 2 players, 919 ids, random opponent)",
+           "value": E * args.vec_steps * world / dt, "unit": "env-steps/s", "envs_per_gpu": E,
+           "steps": args.vec_steps,
+           "with_masked_policy_sampling": {"value": E * n2 / dt2, "unit": "env-steps/s"},
+           "roofline": {"bound": "hbm", "kernel": "k_vec_step", "achieved": achieved / 1e9,
+                        "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                        "kernel_ms": kernel_ms, "bytes_per_unit": VEC_BYTES_PER_STEP, "units_per_launch": E}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2)
+    return out
+
+
+def cpu_baseline_vecenv(seconds: float):
+    """The config-5 env restated on the CPU (oracle/vecenv_oracle.py: C oracle rules, Python
+    loop per env like SyncVectorEnv), random agent + random opponent, 1 core."""
+    from oracle.vecenv_oracle import VecEnvOracle
+
+    ref = VecEnvOracle(64, 7, 4)
+    ref.reset(0)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for e in range(64):
+            ref.step(e, -1)
+        n += 64
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} env steps of 64 sequential 7x7 envs in {dt:.1f} s"}
+
+
 def cpu_baseline_selfplay(seconds: float, model_type: str = "resnet"):
     """Reference-equivalent CPU path: the pure-Python restatement of
     MCTS.simulate (oracle/oracle.py, float64, dict-keyed tree), the C oracle env on 1 host core,
@@ -236,7 +307,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["all", "legal", "selfplay"], default="all")
+    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv"], default="all")
+    ap.add_argument("--envs", type=int, default=8192)
+    ap.add_argument("--vec-steps", type=int, default=1000)
     ap.add_argument("--legal-steps", type=int, default=200)
     ap.add_argument("--legal-warmup", type=int, default=20)
     ap.add_argument("--boards", type=int, default=4096)
@@ -253,6 +326,8 @@ def main():
     world, rank, _ = _dist_init()
     if args.workload == "legal":
         out = bench_legal(args, world, rank)
+    elif args.workload == "vecenv":
+        out = bench_vecenv(args, world, rank)
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
@@ -267,11 +342,15 @@ def main():
             largs.steps, largs.warmup, largs.no_cpu_baseline = args.legal_steps, args.legal_warmup, True
             legal = bench_legal(largs, world, rank)
             out["legal_move"] = {k: legal[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "roofline")}
+            vargs = argparse.Namespace(**vars(args))
+            vargs.no_cpu_baseline = True
+            out["ppo_vector_env"] = bench_vecenv(vargs, world, rank)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_selfplay(args.cpu_seconds, args.model)
             if args.workload == "all":
                 out["cpu_baseline_uninformed"] = cpu_baseline_selfplay(args.cpu_seconds / 2, "dumbnet")
                 out["legal_move"]["cpu_baseline"] = cpu_baseline_legal(legal["_states"], args.cpu_seconds / 2)
+                out["ppo_vector_env"]["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2)
     out.pop("_states", None)
     if rank == 0:
         print(json.dumps(out), flush=True)

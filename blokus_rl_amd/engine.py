@@ -50,6 +50,8 @@ _SIGS = {
     "bk_mcts_root_stats": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "bk_mcts_counters": (_i, [_vp, _vp, _vp]),
     "bk_mcts_leaf_info": (_i, [_vp, _vp, _vp, _vp]),
+    "bk_vec_reset": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
+    "bk_vec_step": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

@@ -169,6 +169,20 @@ int bk_mcts_leaf_info(bk_mcts* m, void* leaf_states, int32_t* depths, void* stre
  * (sum of K over descended nodes), out[7] children created by expansion. */
 int bk_mcts_counters(bk_mcts* m, int64_t* out, void* stream);
 
+/* ---------------------------------------------------------------- config 5: PPO vector env
+ * The blokus_gym `blokus-simple-v0` env as the PPO trainer drives it (ppo/trainer.py:128-175,
+ * :380-386): 2-player preset, the agent is colour 0 against a built-in uniform-random opponent
+ * (colour 1), reward +1 / 0 / -1 at the episode's end, auto-reset. E envs, states [E][384],
+ * rng [E] u64 per-env counters, obs [E][N*N] u8 (0 empty, 1 agent, 2 opponent), mask
+ * [E][mask_words] (the agent's legal ids = `ai_possible_indexes`), reward [E] f32, done [E].
+ * bk_vec_reset: fresh episodes, rng[e] = seeds[e] (seeds NULL keeps rng).
+ * bk_vec_step: actions[e] = the agent's id (< 0, or actions NULL: a uniformly random legal id
+ * drawn in-kernel — the benchmark's policy stand-in); an illegal id ends the episode as a loss. */
+int bk_vec_reset(bk_ctx* ctx, void* states, uint64_t* rng, const uint64_t* seeds, int E, uint8_t* obs,
+                 uint64_t* mask, void* stream);
+int bk_vec_step(bk_ctx* ctx, void* states, uint64_t* rng, const int32_t* actions, int E, uint8_t* obs,
+                uint64_t* mask, float* reward, int32_t* done, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
