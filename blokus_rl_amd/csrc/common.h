@@ -44,6 +44,67 @@ __device__ __forceinline__ uint64_t state_hash(const uint32_t* s) {
   return (uint64_t)s[kWHash] | ((uint64_t)s[kWHash + 1] << 32);
 }
 
+// ---- wave primitives on DPP (row_shr 1/2/4/8, row_bcast 15/31) + readlane: VALU-latency
+// chains instead of ds_bpermute round trips through the LDS crossbar.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+// Generic inclusive wave scan: OP(acc_from_lower, mine) applied in Kogge-Stone order.
+#define BK_WAVE_SCAN(x, DPP, OP)                                 \
+  do {                                                           \
+    const int l_ = lane_id(), rl_ = l_ & 15;                      \
+    auto t_ = DPP<0x111>(x); if (rl_ >= 1) x = OP(t_, x);         \
+    t_ = DPP<0x112>(x); if (rl_ >= 2) x = OP(t_, x);              \
+    t_ = DPP<0x114>(x); if (rl_ >= 4) x = OP(t_, x);              \
+    t_ = DPP<0x118>(x); if (rl_ >= 8) x = OP(t_, x);              \
+    t_ = DPP<0x142>(x); if ((l_ & 31) >= 16) x = OP(t_, x);       \
+    t_ = DPP<0x143>(x); if (l_ >= 32) x = OP(t_, x);              \
+  } while (0)
+
+__device__ __forceinline__ int op_add_i(int a, int b) { return a + b; }
+__device__ __forceinline__ float op_add_f(float a, float b) { return a + b; }
+__device__ __forceinline__ float op_max_f(float a, float b) { return fmaxf(a, b); }
+
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  BK_WAVE_SCAN(x, dpp_i, op_add_i);
+  return x;
+}
+
+__device__ __forceinline__ int readlane_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave-wide results, returned uniform (in every lane).
+__device__ __forceinline__ int wave_sum(int x) {
+  BK_WAVE_SCAN(x, dpp_i, op_add_i);
+  return readlane_i(x, kWave - 1);
+}
+__device__ __forceinline__ float wave_sum_f(float x) {
+  BK_WAVE_SCAN(x, dpp_f, op_add_f);
+  return readlane_f(x, kWave - 1);
+}
+__device__ __forceinline__ float wave_max_f(float x) {
+  BK_WAVE_SCAN(x, dpp_f, op_max_f);
+  return readlane_f(x, kWave - 1);
+}
+
 // Copy a 384-byte state global -> LDS (96 words; lanes 0..63 + 0..31).
 __device__ __forceinline__ void load_state(uint32_t* s, const uint32_t* g) {
   const int l = lane_id();
@@ -116,14 +177,22 @@ __device__ __forceinline__ void build_mask(const DevPreset& dp, const uint32_t* 
     for (int pc = 0; pc < dp.num_pieces; ++pc) {
       if (!((pieces >> pc) & 1u)) continue;  // wave-uniform
       const int end = dp.piece_item_off[pc + 1];
-      for (int i = dp.piece_item_off[pc] + l; i < end; i += kWave) {
-        const uint64_t it = dp.items[i];
-        const uint32_t v = eval_item(it, fa);
-        if (v) {
-          const int base = item_base(it);
-          const int w = base >> 5, sh = base & 31;
-          atomicOr(&m32[w], v << sh);
-          if (sh + item_W(it) > 32) atomicOr(&m32[w + 1], v >> (32 - sh));
+      // four items per lane per trip: their LDS row reads and shifts are independent chains
+      for (int i0 = dp.piece_item_off[pc] + l; i0 < end; i0 += 4 * kWave) {
+        uint64_t it[4];
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) it[u] = i0 + u * kWave < end ? dp.items[i0 + u * kWave] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i0 + u * kWave < end ? eval_item(it[u], fa) : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (v[u]) {
+            const int base = item_base(it[u]);
+            const int w = base >> 5, sh = base & 31;
+            atomicOr(&m32[w], v[u] << sh);
+            if (sh + item_W(it[u]) > 32) atomicOr(&m32[w + 1], v[u] >> (32 - sh));
+          }
         }
       }
     }
@@ -140,10 +209,11 @@ __device__ __forceinline__ bool has_any_legal(const DevPreset& dp, const uint32_
   for (int pc = 0; pc < dp.num_pieces; ++pc) {
     if (!((pieces >> pc) & 1u)) continue;
     const int beg = dp.piece_item_off[pc], end = dp.piece_item_off[pc + 1];
-    for (int i0 = beg; i0 < end; i0 += kWave) {
-      const int i = i0 + l;
-      uint32_t v = 0;
-      if (i < end) v = eval_item(dp.items[i], fa);
+    for (int i0 = beg + l; i0 - l < end; i0 += 2 * kWave) {  // two items per lane per trip
+      const int i1 = i0 + kWave;
+      const uint64_t a0 = i0 < end ? dp.items[i0] : 0ull;
+      const uint64_t a1 = i1 < end ? dp.items[i1] : 0ull;
+      const uint32_t v = (i0 < end ? eval_item(a0, fa) : 0u) | (i1 < end ? eval_item(a1, fa) : 0u);
       if (__ballot(v != 0u)) return true;
     }
   }
@@ -184,12 +254,11 @@ __device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, in
       s[p * kMaxN + row] = nw;
     }
   }
-  // xor-reduce lanes 0..7
-  hx ^= __shfl_xor(hx, 1, 8);
-  hx ^= __shfl_xor(hx, 2, 8);
-  hx ^= __shfl_xor(hx, 4, 8);
+  // xor-reduce lanes 0..4 (scalar reads)
+  const uint64_t hsum = readlane_u64(hx, 0) ^ readlane_u64(hx, 1) ^ readlane_u64(hx, 2) ^ readlane_u64(hx, 3) ^
+                        readlane_u64(hx, 4);
   if (l == 0) {
-    const uint64_t h = state_hash(s) ^ hx;
+    const uint64_t h = state_hash(s) ^ hsum;
     s[kWHash] = (uint32_t)h;
     s[kWHash + 1] = (uint32_t)(h >> 32);
     s[kWPieces + p] &= ~(1u << pc);
@@ -226,22 +295,6 @@ __device__ __forceinline__ void terminal_scores(const DevPreset& dp, const uint3
   for (int k = 0; k < dp.P; ++k) out[k] = sq[k] == best ? (nwin == 1 ? 3.0 : 1.0) : -1.0;
 }
 
-__device__ __forceinline__ int wave_incl_scan(int x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(x, o, kWave);
-    if (l >= o) x += y;
-  }
-  return x;
-}
-
-__device__ __forceinline__ int wave_sum(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
-  return x;
-}
-
 // Write the legal ids of LDS mask m32 in ascending order to ids[0..cap); returns K.
 __device__ __forceinline__ int compact_ids(const DevPreset& dp, const uint32_t* m32, int32_t* ids, int cap) {
   const int l = lane_id();
@@ -258,7 +311,7 @@ __device__ __forceinline__ int compact_ids(const DevPreset& dp, const uint32_t* 
       if (pos < cap) ids[pos] = w * 32 + b;
       ++pos;
     }
-    total += __shfl(incl, kWave - 1, kWave);
+    total += readlane_i(incl, kWave - 1);
   }
   return total;
 }

@@ -78,6 +78,48 @@ __device__ __forceinline__ void orient_all(const DevPreset& dp, const RowCtx& c,
   (orient_step<(int)Os, WPB, SPLIT>(dp, c, wave, base), ...);
 }
 
+// One board per wave (the state already in LDS): lanes 0..N-1 are the board's rows, the same
+// unrolled orientation steps as below, the bitmask ORed into m32 (zeroed here). Replaces the
+// item loop wherever a single wave owns a single board (k_select's leaf, k_legal_ids, ...).
+__device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32) {
+  const int l = lane_id();
+  const int N = dp.N;
+  for (int i = l; i < dp.W32pad / 4; i += kWave) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const bool ok = l < N;
+  const int r = ok ? l : 0;
+  const uint32_t own = ok ? s[q * kMaxN + r] : 0u;
+  const uint32_t occ = ok ? (s[r] | s[kMaxN + r] | s[2 * kMaxN + r] | s[3 * kMaxN + r]) : 0u;
+  const uint32_t up = (ok && r > 0) ? s[q * kMaxN + r - 1] : 0u;
+  const uint32_t dn = (ok && r + 1 < N) ? s[q * kMaxN + r + 1] : 0u;
+  const bool first = __ballot(own != 0u) == 0ull;
+  uint32_t forb = 0u, anch = 0u;
+  if (ok) {
+    forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
+    if (first)
+      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+    else
+      anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
+  }
+  RowCtx c;
+  c.fr[0] = __brev(forb);
+  c.ar[0] = __brev(anch);
+#pragma unroll
+  for (int d = 1; d < 5; ++d) {
+    const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
+    c.fr[d] = __shfl(c.fr[0], src, kWave);
+    c.ar[d] = __shfl(c.ar[0], src, kWave);
+  }
+  c.r = r;
+  c.rN1 = r * (N + 1);
+  c.pieces = s[kWPieces + q];
+#pragma unroll
+  for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
+  c.mb = m32;
+  __syncthreads();
+  orient_all<1, 0>(dp, c, 0, std::make_index_sequence<kNumOrient>{});
+  __syncthreads();
+}
+
 // Workgroup = WPB waves sharing one group of boards_per_wave boards: wave w evaluates the
 // orientations O with O % WPB == w (round robin keeps the cell work balanced), all OR into the
 // same LDS masks, then the WPB waves stream the masks out together.

@@ -20,10 +20,23 @@
 
 #include "../../include/blokus_engine.h"
 #include "ctx.h"
+#include "legal_rows.h"
 
 namespace bk {
 
-constexpr int kMaxDepth = 96;  // > 84 = most placements a 4-player game can still make
+constexpr int kMaxDepth = 96;
+constexpr int kExpandLdsIds = 2048;  // leaf ids staged in LDS up to this K
+constexpr int kGatherRegs = 16;      // logits gathered into registers: K <= 1024 in one round
+
+// Diagnostic build only (-DBK_STAMPS, `make diag`): per-tree s_memtime stamps at phase
+// boundaries of k_select / k_expand_backup; never compiled into the shipped library.
+#ifdef BK_STAMPS
+__device__ unsigned long long g_stamps[2][4096][8];
+#define BK_STAMP(k, i) \
+  do { if (lane_id() == 0 && blockIdx.x < 4096) g_stamps[k][blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BK_STAMP(k, i) do { } while (0)
+#endif  // > 84 = most placements a 4-player game can still make
 
 struct DevMcts {
   int T, node_cap, TS;  // TS = table slots per tree (power of two)
@@ -71,12 +84,12 @@ __device__ __forceinline__ int table_find(const DevMcts& m, int t, uint64_t key,
     const uint64_t emp = __ballot(k == 0ull);
     if (hit) {
       const int src = __ffsll((unsigned long long)hit) - 1;
-      const int slot_hit = __shfl((int)slot, src, kWave);
+      const int slot_hit = readlane_i((int)slot, src);
       return m.tab_node[(size_t)t * m.TS + slot_hit];
     }
     if (emp) {
       const int src = __ffsll((unsigned long long)emp) - 1;
-      if (free_slot) *free_slot = __shfl((int)slot, src, kWave);
+      if (free_slot) *free_slot = readlane_i((int)slot, src);
       return -1;
     }
   }
@@ -85,13 +98,28 @@ __device__ __forceinline__ int table_find(const DevMcts& m, int t, uint64_t key,
 }
 
 // argmax over (value, index): larger value wins, ties -> smaller index (np.argmax's first max).
+// DPP prefix-argmax; lane 63 ends with the wave's argmax, returned uniform.
 __device__ __forceinline__ void wave_argmax(double& best, int& bi) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double ob = __shfl_xor(best, o, kWave);
-    const int oi = __shfl_xor(bi, o, kWave);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  const int l = lane_id(), rl = l & 15;
+#define BK_ARGMAX_STEP(CTRL, COND)                                 \
+  {                                                               \
+    const double tb = dpp_d<CTRL>(best);                          \
+    const int ti = dpp_i<CTRL>(bi);                               \
+    if ((COND) && (tb > best || (tb == best && ti < bi))) {        \
+      best = tb;                                                  \
+      bi = ti;                                                    \
+    }                                                             \
   }
+  BK_ARGMAX_STEP(0x111, rl >= 1)
+  BK_ARGMAX_STEP(0x112, rl >= 2)
+  BK_ARGMAX_STEP(0x114, rl >= 4)
+  BK_ARGMAX_STEP(0x118, rl >= 8)
+  BK_ARGMAX_STEP(0x142, (l & 31) >= 16)
+  BK_ARGMAX_STEP(0x143, l >= 32)
+#undef BK_ARGMAX_STEP
+  bi = readlane_i(bi, kWave - 1);
+  const uint64_t u = readlane_u64((uint64_t)__double_as_longlong(best), kWave - 1);
+  best = __longlong_as_double((long long)u);
 }
 
 // PUCT choice at a node (mcts.py:41-46): argmax_i Q_i + cpuct*P_i*sqrt(sum N + 1e-6)/(1+N_i).
@@ -100,13 +128,25 @@ __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K
   const double sq = sqrt((double)visits + 1e-6);
   double best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int i = l; i < K; i += kWave) {
-    const double u = ((cp * (double)m.ch_P[off + i]) * sq) / (1.0 + (double)m.ch_N[off + i]);
-    const double hv = m.ch_Q[off + i] + u;
-    if (hv > best) { best = hv; bi = i; }
+  const float* P = m.ch_P + off;
+  const uint32_t* Nn = m.ch_N + off;
+  const double* Q = m.ch_Q + off;
+  int i = l;
+  for (; i + kWave < K; i += 2 * kWave) {  // two children per lane per trip: loads overlap
+    const float p0 = P[i], p1 = P[i + kWave];
+    const uint32_t n0 = Nn[i], n1 = Nn[i + kWave];
+    const double q0 = Q[i], q1 = Q[i + kWave];
+    const double h0 = q0 + ((cp * (double)p0) * sq) / (1.0 + (double)n0);
+    const double h1 = q1 + ((cp * (double)p1) * sq) / (1.0 + (double)n1);
+    if (h0 > best) { best = h0; bi = i; }
+    if (h1 > best) { best = h1; bi = i + kWave; }
+  }
+  if (i < K) {
+    const double h = Q[i] + ((cp * (double)P[i]) * sq) / (1.0 + (double)Nn[i]);
+    if (h > best) { best = h; bi = i; }
   }
   wave_argmax(best, bi);
-  return __shfl(bi, 0, kWave);
+  return bi;
 }
 
 __global__ __launch_bounds__(64) void k_reset(DevMcts m, const int32_t* flags) {
@@ -133,8 +173,10 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
     for (int i = l; i < obs_len; i += kWave) obs[(size_t)t * obs_len + i] = 0.0f;
     return;
   }
+  BK_STAMP(0, 0);
   load_state(s, roots + (size_t)t * kStateWords);
   __syncthreads();
+  BK_STAMP(0, 1);
   double cp = cpuct;
   int depth = 0, err = 0;
   long long scanned = 0;
@@ -158,6 +200,7 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
     ++depth;
     cp = 1.0;  // the recursive call of mcts.py:50 passes no cpuct
   }
+  BK_STAMP(0, 2);
   int status;
   float* o = obs + (size_t)t * obs_len;
   if (err) {
@@ -167,7 +210,8 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
     if (l == 0) terminal_scores(dp, s, m.leaf_scores + (size_t)t * kMaxP);
   } else {
     status = 1;
-    build_mask(dp, s, (int)s[kWToMove], fa, m32);
+    build_mask_rows(dp, s, (int)s[kWToMove], m32);
+    BK_STAMP(0, 3);
     uint64_t* mo = m.leaf_mask + (size_t)t * dp.W64;
     uint64_t* mo2 = mask_out ? mask_out + (size_t)t * dp.W64 : nullptr;
     for (int j = l; j < dp.W64; j += kWave) {
@@ -177,22 +221,25 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
     }
     store_state(m.leaf_state + (size_t)t * kStateWords, s);
   }
-  // observation row (zeros unless the leaf needs the net)
-  const int NN = dp.N * dp.N;
+  BK_STAMP(0, 4);
+  // observation row (zeros unless the leaf needs the net): lane = (plane, board row), the row's
+  // N floats as float4 stores when N is a multiple of 4 (no per-cell index arithmetic)
   const int tm = (int)s[kWToMove];
-  for (int i = l; i < obs_len; i += kWave) {
-    float v = 0.0f;
-    if (status == 1) {
-      const int plane = i / NN, cell = i - plane * NN;
-      if (plane < dp.P) {
-        const int r = cell / dp.N, c = cell - r * dp.N;
-        v = (float)((s[plane * kMaxN + r] >> c) & 1u);
-      } else {
-        v = (plane - dp.P) == tm ? 1.0f : 0.0f;
-      }
+  const int rows = 2 * dp.P * dp.N;
+  for (int pr = l; pr < rows; pr += kWave) {
+    const int plane = pr / dp.N, r = pr - plane * dp.N;
+    uint32_t bits = 0u;
+    if (status == 1) bits = plane < dp.P ? s[plane * kMaxN + r] : ((plane - dp.P) == tm ? dp.full_row : 0u);
+    float* dst = o + pr * dp.N;
+    if ((dp.N & 3) == 0) {
+      for (int c = 0; c < dp.N; c += 4)
+        *reinterpret_cast<float4*>(dst + c) = make_float4((float)((bits >> c) & 1u), (float)((bits >> (c + 1)) & 1u),
+                                                          (float)((bits >> (c + 2)) & 1u), (float)((bits >> (c + 3)) & 1u));
+    } else {
+      for (int c = 0; c < dp.N; ++c) dst[c] = (float)((bits >> c) & 1u);
     }
-    o[i] = v;
   }
+  BK_STAMP(0, 5);
   if (l == 0) {
     m.leaf_status[t] = status;
     status_out[t] = status;
@@ -217,6 +264,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
   const int l = lane_id();
   const int status = m.leaf_status[t];
   if (status == 0) return;
+  BK_STAMP(1, 0);
   if (status == 1) {
     const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
     for (int j = l; j < dp.W64; j += kWave) {
@@ -230,9 +278,16 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
     const int64_t used = m.tree_children[t];
     const int64_t room = m.child_cap_per_tree - used;
     const int64_t off = (int64_t)t * m.child_cap_per_tree + used;
-    // legal ids, ascending (np.where order, mcts.py:64), straight into the child region
-    const int K = compact_ids(dp, m32, m.ch_id + off, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
+    // legal ids, ascending (np.where order, mcts.py:64): into LDS when K fits, else straight
+    // into the tree's child region
+    int32_t* ids_lds = reinterpret_cast<int32_t*>(m32 + dp.W32pad);
+    const int cap_lds = kExpandLdsIds;
+    BK_STAMP(1, 1);
+    int K = compact_ids(dp, m32, ids_lds, cap_lds);
+    const bool in_lds = K <= cap_lds;
+    if (!in_lds) K = compact_ids(dp, m32, m.ch_id + off, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
     __syncthreads();
+    BK_STAMP(1, 2);
     if (node >= m.node_cap) err |= kErrTable;
     if (K > room) err |= kErrChildPool;
     int free_slot = -1;
@@ -241,30 +296,50 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
       const int found = table_find(m, t, key, &free_slot);
       if (found >= 0 || free_slot < 0) err |= kErrTable;
     }
+    BK_STAMP(1, 3);
     if (!err) {
       const float* lp = logp + (size_t)t * dp.A;
-      const int32_t* cid = m.ch_id + off;
+      const int32_t* cid = in_lds ? ids_lds : m.ch_id + off;
+      // all of a lane's gathers issued before any is used (K <= 64 * kGatherRegs)
+      float x[kGatherRegs];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < kGatherRegs; ++j) {
+        const int i = l + j * kWave;
+        x[j] = i < K ? lp[cid[i]] : -INFINITY;
+      }
+#pragma unroll
+      for (int j = 0; j < kGatherRegs; ++j) mx = fmaxf(mx, x[j]);
+      for (int i = l + kGatherRegs * kWave; i < K; i += kWave) mx = fmaxf(mx, lp[cid[i]]);
+      float lse = 0.0f;
       if (prior_mode == 0) {
-        float mx = -INFINITY;
-        for (int i = l; i < K; i += kWave) mx = fmaxf(mx, lp[cid[i]]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, kWave));
+        mx = wave_max_f(mx);
         float sum = 0.0f;
-        for (int i = l; i < K; i += kWave) sum += expf(lp[cid[i]] - mx);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
-        const float lse = logf(sum);
-        for (int i = l; i < K; i += kWave) {
+        for (int j = 0; j < kGatherRegs; ++j) sum += l + j * kWave < K ? expf(x[j] - mx) : 0.0f;
+        for (int i = l + kGatherRegs * kWave; i < K; i += kWave) sum += expf(lp[cid[i]] - mx);
+        sum = wave_sum_f(sum);
+        lse = logf(sum);
+#pragma unroll
+        for (int j = 0; j < kGatherRegs; ++j) x[j] = expf((x[j] - mx) - lse);
+      }
+      // coalesced child initialisation: child i = (id, N 0, Q 0, P)
+#pragma unroll
+      for (int j = 0; j < kGatherRegs; ++j) {
+        const int i = l + j * kWave;
+        if (i < K) {
+          if (in_lds) m.ch_id[off + i] = cid[i];
           m.ch_N[off + i] = 0u;
           m.ch_Q[off + i] = 0.0;
-          m.ch_P[off + i] = expf((lp[cid[i]] - mx) - lse);
+          m.ch_P[off + i] = x[j];
         }
-      } else {
-        for (int i = l; i < K; i += kWave) {
-          m.ch_N[off + i] = 0u;
-          m.ch_Q[off + i] = 0.0;
-          m.ch_P[off + i] = lp[cid[i]];
-        }
+      }
+      for (int i = l + kGatherRegs * kWave; i < K; i += kWave) {
+        const float xi = lp[cid[i]];
+        if (in_lds) m.ch_id[off + i] = cid[i];
+        m.ch_N[off + i] = 0u;
+        m.ch_Q[off + i] = 0.0;
+        m.ch_P[off + i] = prior_mode == 0 ? expf((xi - mx) - lse) : xi;
       }
       if (l == 0) {
         const size_t gn = (size_t)t * m.node_cap + node;
@@ -285,6 +360,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
   } else {
     if (l < dp.P) vsh[l] = m.leaf_scores[(size_t)t * kMaxP + l];
   }
+  BK_STAMP(1, 4);
   __syncthreads();
   const int depth = m.depth[t];
   for (int d = l; d < depth; d += kWave) {
@@ -297,6 +373,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
     m.ch_N[ci] = n + 1u;
     m.node_visits[(size_t)t * m.node_cap + m.path_node[pi]] += 1u;
   }
+  BK_STAMP(1, 5);
 }
 
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
@@ -347,7 +424,6 @@ __global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restri
       if (v > best) { best = v; bi = i; }
     }
     wave_argmax(best, bi);
-    bi = __shfl(bi, 0, kWave);
     for (int i = l; i < Kc; i += kWave) o[i] = i == bi ? 1.0 : 0.0;
     return;
   }
@@ -389,6 +465,12 @@ static int mcts_alloc(bk_mcts* m, T** p, size_t count) {
 }
 
 extern "C" {
+
+#ifdef BK_STAMPS
+int bk_debug_stamps(unsigned long long* out) {  // [2][4096][8] host copy
+  return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)), "stamps");
+}
+#endif
 
 int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_mcts** out) {
   BK_REQUIRE(ctx && out && trees > 0 && node_cap > 0 && child_cap >= trees, "bad argument");
@@ -465,7 +547,7 @@ int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double 
 int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, int prior_mode, void* stream) {
   BK_REQUIRE(m && logp && values && (prior_mode == 0 || prior_mode == 1), "bad argument");
   const DevPreset& dp = m->ctx->dp;
-  const size_t lds = sizeof(uint32_t) * (size_t)dp.W32pad;
+  const size_t lds = sizeof(uint32_t) * ((size_t)dp.W32pad + kExpandLdsIds);
   hipLaunchKernelGGL(k_expand_backup, dim3(m->d.T), dim3(kWave), lds, (hipStream_t)stream, dp, m->d, logp, values,
                      prior_mode);
   return launch_check("k_expand_backup");

@@ -35,7 +35,7 @@ __device__ __forceinline__ int kth_legal(const DevPreset& dp, const uint32_t* m3
     const uint32_t bits = w < dp.W32 ? m32[w] : 0u;
     const int cnt = __popc(bits);
     const int incl = wave_incl_scan(cnt);
-    const int total = __shfl(incl, kWave - 1, kWave);
+    const int total = readlane_i(incl, kWave - 1);
     if (k < before + total) {  // wave-uniform
       const int excl = before + incl - cnt;
       int found = -1;
@@ -45,7 +45,7 @@ __device__ __forceinline__ int kth_legal(const DevPreset& dp, const uint32_t* m3
         found = w * 32 + __ffs(b) - 1;
       }
       const uint64_t who = __ballot(found >= 0);
-      return __shfl(found, __ffsll((unsigned long long)who) - 1, kWave);
+      return readlane_i(found, __ffsll((unsigned long long)who) - 1);
     }
     before += total;
   }

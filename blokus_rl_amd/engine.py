@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libblokus_hip.so")
+LIB_PATH = os.environ.get("BK_LIB") or os.path.join(HERE, "_lib", "libblokus_hip.so")
 STATE_BYTES = 384
 STATE_WORDS = STATE_BYTES // 4
 

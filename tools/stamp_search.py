@@ -1,0 +1,32 @@
+"""Diagnostic: per-phase cycle shares of k_select / k_expand_backup from the BK_STAMPS build
+(BK_LIB=blokus_rl_amd/_lib/diag/libblokus_hip_diag.so). Runs uninformed self-play plies."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from blokus_rl_amd import engine
+from blokus_rl_amd.engine import Engine
+from blokus_rl_amd.nets import DumbNet
+from blokus_rl_amd.alphazero.selfplay import SelfPlay
+
+eng = Engine(20, 4, 5)
+sp = SelfPlay(eng, DumbNet(20, 4, eng.A), 256, num_sims=100, seed=0, continuous=True)
+sp.play_ply(); sp.play_ply()
+lib = engine.load_library()
+lib.bk_debug_stamps.argtypes = [ctypes.c_void_p]
+acc = {0: [], 1: []}
+for _ in range(30):
+    sp.simulate()
+    torch.cuda.synchronize()
+    buf = np.zeros((2, 4096, 8), dtype=np.uint64)
+    assert lib.bk_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p)) == 0
+    for k in (0, 1):
+        acc[k].append(buf[k, :256].astype(np.int64))
+for k, names in ((0, ["load", "descent", "build_mask", "mask+state store", "obs write"]),
+                 (1, ["mask load", "compact", "table", "softmax+init", "backup"])):
+    a = np.stack(acc[k])  # [iters, T, 8]
+    d = np.diff(a[:, :, :6], axis=2)
+    tot = a[:, :, 5] - a[:, :, 0]
+    print(["k_select", "k_expand_backup"][k], "median total cycles", int(np.median(tot)),
+          "(s_memtime ticks)")
+    for i, n in enumerate(names):
+        print(f"   {n:18s} median {int(np.median(d[:, :, i])):8d}  mean {d[:, :, i].mean():10.0f}")
