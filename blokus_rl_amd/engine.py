@@ -52,6 +52,11 @@ _SIGS = {
     "bk_mcts_leaf_info": (_i, [_vp, _vp, _vp, _vp]),
     "bk_vec_reset": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "bk_vec_step": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "bk_replay_stride": (ctypes.c_size_t, [_i]),
+    "bk_replay_batch": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bk_policy_loss": (_i, [_vp, ctypes.c_int64, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "bk_policy_loss_grad": (_i, [_vp, ctypes.c_int64, _vp, _vp, _vp, _i, _i, _vp, ctypes.c_float, _vp, _vp,
+                                 ctypes.c_int64, _vp]),
 }
 
 _LIB = None
@@ -200,6 +205,29 @@ class Engine:
         if out is None:
             out = torch.empty((B,) + self.obs_shape, dtype=torch.float32, device=self.device)
         _check(self.lib.bk_observe(self.h, _ptr(states), B, _ptr(out), self._s()))
+        return out
+
+    def replay_batch(self, rows: torch.Tensor, cap: int, index: torch.Tensor, with_states: bool = False):
+        """Packed replay rows [E, stride] (uint8, device) + index [B] int64 -> the training batch
+        {observation [B,2P,N,N] f32, ids [B,cap] int16, pi [B,cap] f32, k [B] int32,
+        score [B,P] f32 (, states [B,384])} (bk_replay_batch)."""
+        B = index.shape[0]
+        dev = self.device
+        assert rows.dtype == torch.uint8 and rows.shape[1] == self.lib.bk_replay_stride(cap)
+        index = index.to(device=dev, dtype=torch.int64).contiguous()
+        out = {
+            "observation": torch.empty((B,) + self.obs_shape, dtype=torch.float32, device=dev),
+            "ids": torch.empty((B, cap), dtype=torch.int16, device=dev),
+            "pi": torch.empty((B, cap), dtype=torch.float32, device=dev),
+            "k": torch.empty(B, dtype=torch.int32, device=dev),
+            "score": torch.empty((B, self.P), dtype=torch.float32, device=dev),
+        }
+        st = self.empty_states(B) if with_states else None
+        _check(self.lib.bk_replay_batch(self.h, _ptr(rows), cap, _ptr(index), B, _ptr(out["observation"]),
+                                        _ptr(out["ids"]), _ptr(out["pi"]), _ptr(out["k"]), _ptr(out["score"]),
+                                        _ptr(st), self._s()))
+        if with_states:
+            out["states"] = st
         return out
 
     def square_counts(self, states: torch.Tensor) -> torch.Tensor:

@@ -19,6 +19,7 @@
 #ifndef BLOKUS_ENGINE_H
 #define BLOKUS_ENGINE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -182,6 +183,33 @@ int bk_vec_reset(bk_ctx* ctx, void* states, uint64_t* rng, const uint64_t* seeds
                  uint64_t* mask, void* stream);
 int bk_vec_step(bk_ctx* ctx, void* states, uint64_t* rng, const int32_t* actions, int E, uint8_t* obs,
                 uint64_t* mask, float* reward, int32_t* done, void* stream);
+
+/* ---------------------------------------------------------------- learner
+ * Packed replay row (blokus_rl_amd/replay.py), fixed stride bk_replay_stride(cap), 16-B aligned:
+ *   state 384 B | K int32 | player int32 | z f32[4] | ids int16[cap] (ascending legal ids, -1
+ *   padded) | pi f32[cap].  cap is a multiple of 64. */
+size_t bk_replay_stride(int cap);
+
+/* The training-batch loader: replaces AlphaZeroDataset.__getitem__ + collate_dataset_fn
+ * (alphazero/dataset.py:38-54) and train_step's host->device copy (neural_network.py:64).
+ * For b < B, row index[b] of `rows` -> obs[b][2P][N][N] f32 (the get_observation planes),
+ * ids[b][cap], pi[b][cap], k[b], z[b][P]; states[b][384] too when states != NULL. */
+int bk_replay_batch(bk_ctx* ctx, const void* rows, int cap, const int64_t* index, int B, float* obs,
+                    int16_t* ids, float* pi, int32_t* k, float* z, void* states, void* stream);
+
+/* Policy term of BlokusNNetWrapper.compute_loss (neural_network.py:138-157, with
+ * get_valid_dist(log_softmax=True), :159-173) over sparse search policies: for each row b,
+ * loss[b] = -sum_{j<k[b]} pi[b][j] * log_softmax(x[b][ids[b][0..k[b])])_j and lse[b] = the
+ * log-partition of the row's legal logits. x is [B][ldx] f32 (the net's policy output). */
+int bk_policy_loss(const float* x, int64_t ldx, const int16_t* ids, const float* pi, const int32_t* k, int cap,
+                   int B, float* loss, float* lse, void* stream);
+
+/* Its gradient: grad[b][ids[b][j]] = s * (S_b * exp(x[b][ids[b][j]] - lse[b]) - pi[b][j]),
+ * S_b = sum_j pi[b][j], s = scale * (*gscale) (gscale: a device f32, the upstream gradient, or
+ * NULL for 1); entries at other ids are left untouched (the caller zero-fills). */
+int bk_policy_loss_grad(const float* x, int64_t ldx, const int16_t* ids, const float* pi, const int32_t* k,
+                        int cap, int B, const float* lse, float scale, const float* gscale, float* grad,
+                        int64_t ldg, void* stream);
 
 #ifdef __cplusplus
 }

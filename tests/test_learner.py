@@ -1,0 +1,285 @@
+"""Learner path: the policy loss against the reference's compute_loss
+(tests/golden/loss_golden.npz, made by tests/golden/make_loss_golden.py from
+neural_network.py:138-157), the device batch loader against bk_observe + the packed rows, and
+the DDP sharding (gloo, world 2, CPU)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+from make_loss_golden import logits_row  # noqa: E402
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "loss_golden.npz"))
+
+
+def golden_case(tag, device="cpu"):
+    A = int(GOLD[f"{tag}_A"])
+    seeds = GOLD[f"{tag}_seeds"]
+    k = GOLD[f"{tag}_k"]
+    B = len(k)
+    cap = max(64, (int(k.max()) + 63) // 64 * 64)
+    ids = np.full((B, cap), -1, np.int16)
+    pi = np.zeros((B, cap), np.float32)
+    off = np.concatenate([[0], np.cumsum(k)])
+    for b in range(B):
+        ids[b, : k[b]] = GOLD[f"{tag}_ids"][off[b]:off[b + 1]]
+        pi[b, : k[b]] = GOLD[f"{tag}_pi"][off[b]:off[b + 1]]
+    logits = np.stack([logits_row(int(s), A) for s in seeds])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    return {
+        "A": A, "B": B, "off": off, "logits": t(logits), "ids": t(ids), "pi": t(pi),
+        "k": t(k.astype(np.int32)), "v_pred": t(GOLD[f"{tag}_v_pred"]), "v_gt": t(GOLD[f"{tag}_v_gt"]),
+        "loss": float(GOLD[f"{tag}_loss"]), "grad_p": GOLD[f"{tag}_grad_p"], "grad_v": GOLD[f"{tag}_grad_v"],
+    }
+
+
+def torch_sparse_policy_loss(x, ids, pi, k):
+    """The same function as bk_policy_loss, in plain torch (CPU restatement for the DDP test)."""
+    B, cap = ids.shape
+    valid = torch.arange(cap, device=x.device).unsqueeze(0) < k.long().unsqueeze(1)
+    g = torch.gather(x, 1, ids.long().clamp(min=0))
+    g = g.masked_fill(~valid, float("-inf"))
+    lsm = torch.log_softmax(g, dim=1)
+    lsm = torch.where(valid, lsm, torch.zeros_like(lsm))
+    return -(pi * lsm).sum() / B
+
+
+@pytest.mark.parametrize("tag", ["c7", "c20"])
+def test_dropin_compute_loss_matches_reference(tag):
+    """The drop-in compute_loss (dense masks) and the sparse restatement both reproduce the
+    reference's loss and gradients."""
+    from blokus_rl_amd.neural_network import BlokusNNetWrapper
+
+    c = golden_case(tag)
+    masks = torch.zeros((c["B"], c["A"]), dtype=torch.bool)
+    for b in range(c["B"]):
+        masks[b, c["ids"][b, : int(c["k"][b])].long()] = True
+    x = c["logits"].clone().requires_grad_(True)
+    v = c["v_pred"].clone().requires_grad_(True)
+    w = BlokusNNetWrapper.__new__(BlokusNNetWrapper)
+    loss = w.compute_loss(masks, (x, v), (c["pi"], c["v_gt"]))
+    loss.backward()
+    assert abs(loss.item() - c["loss"]) <= 1e-5 * max(1.0, abs(c["loss"]))
+    gs = np.concatenate([x.grad[b, c["ids"][b, : int(c["k"][b])].long()].numpy() for b in range(c["B"])])
+    np.testing.assert_allclose(gs, c["grad_p"], atol=1e-7, rtol=1e-5)
+    np.testing.assert_allclose(v.grad.numpy(), c["grad_v"], atol=1e-7, rtol=1e-5)
+    x2 = c["logits"].clone().requires_grad_(True)
+    l2 = torch_sparse_policy_loss(x2, c["ids"], c["pi"], c["k"]) + (c["v_pred"].squeeze() - c["v_gt"]).pow(2).mean()
+    assert abs(l2.item() - c["loss"]) <= 1e-5 * max(1.0, abs(c["loss"]))
+
+
+def test_replay_stride_matches_library():
+    from blokus_rl_amd import replay
+    from blokus_rl_amd.engine import load_library
+
+    lib = load_library()
+    for cap in (64, 128, 704, 1024):
+        assert lib.bk_replay_stride(cap) == replay.stride_of(cap)
+
+
+# ---------------------------------------------------------------- DDP (gloo, CPU)
+class _TinyNet(torch.nn.Module):
+    """A BN-free stand-in net (so single-process and 2-rank DDP steps are the same function)."""
+
+    def __init__(self, P=4, N=20, A=30433):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(2 * P, 4, 3, padding=1)
+        self.pol = torch.nn.Linear(4 * N * N, A)
+        self.val = torch.nn.Linear(4 * N * N, P)
+
+    def forward(self, x):
+        h = torch.relu(self.conv(x)).flatten(1)
+        return torch.log_softmax(self.pol(h), 1), torch.tanh(self.val(h))
+
+
+def _cpu_batch(B, seed, cap=64, P=4, N=20, A=30433):
+    g = torch.Generator().manual_seed(seed)
+    k = torch.randint(1, cap, (B,), generator=g, dtype=torch.int32)
+    ids = torch.full((B, cap), -1, dtype=torch.int16)
+    pi = torch.zeros((B, cap))
+    for b in range(B):
+        kk = int(k[b])
+        ids[b, :kk] = torch.sort(torch.randperm(A, generator=g)[:kk]).values.to(torch.int16)
+        p = torch.rand(kk, generator=g)
+        pi[b, :kk] = p / p.sum()
+    obs = (torch.rand((B, 2 * P, N, N), generator=g) < 0.3).float()
+    z = torch.randint(-1, 2, (B, P), generator=g).float()
+    return {"observation": obs, "ids": ids, "pi": pi, "k": k, "score": z}
+
+
+def _ddp_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from blokus_rl_amd.alphazero.learner import Learner
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    net = _TinyNet()
+    L = Learner(net, lr=1e-3, weight_decay=1e-4, batch_size=8, policy_fn=torch_sparse_policy_loss)
+    full = _cpu_batch(16, 5)
+    half = {k: v[rank * 8:(rank + 1) * 8] for k, v in full.items()}
+    L.train_step(half)
+    sh = L.epoch_indices(40)
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}, sh.tolist()))
+    dist.destroy_process_group()
+
+
+def test_ddp_two_ranks_equal_single_process():
+    """Two gloo ranks on halves of a batch == one process on the whole batch (gradients are
+    averaged by DDP, the loss is a per-row mean); the epoch shards are disjoint and equal-sized."""
+    import torch.multiprocessing as mp
+
+    from blokus_rl_amd.alphazero.learner import Learner
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29631
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (sd, sh)) for r, sd, sh in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    net = _TinyNet()
+    L = Learner(net, lr=1e-3, weight_decay=1e-4, batch_size=16, policy_fn=torch_sparse_policy_loss)
+    L.train_step(_cpu_batch(16, 5))
+    for name, ref in net.state_dict().items():
+        for r in (0, 1):
+            torch.testing.assert_close(torch.from_numpy(res[r][0][name]), ref, rtol=1e-5, atol=1e-6)
+    s0, s1 = res[0][1], res[1][1]
+    assert len(s0) == len(s1) == 20 and not set(s0) & set(s1)
+
+
+# ---------------------------------------------------------------- GPU (HIP kernels)
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["c7", "c20"])
+def test_hip_policy_loss_matches_reference(tag):
+    from blokus_rl_amd.alphazero.learner import alphazero_loss
+
+    c = golden_case(tag, "cuda")
+    x = c["logits"].clone().requires_grad_(True)
+    v = c["v_pred"].clone().requires_grad_(True)
+    batch = {"ids": c["ids"], "pi": c["pi"], "k": c["k"], "score": c["v_gt"]}
+    loss = alphazero_loss(x, v, batch)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - c["loss"]) <= 2e-5 * max(1.0, abs(c["loss"]))
+    g = x.grad.cpu()
+    gs = np.concatenate([g[b, c["ids"][b, : int(c["k"][b])].long().cpu()].numpy() for b in range(c["B"])])
+    np.testing.assert_allclose(gs, c["grad_p"], atol=2e-7, rtol=2e-5)
+    np.testing.assert_allclose(v.grad.cpu().numpy(), c["grad_v"], atol=1e-7, rtol=1e-5)
+    # zero off the legal ids (the reference's gradient is too, asserted by the generator)
+    nz = int((g != 0).sum())
+    assert nz <= int(c["k"].sum())
+
+
+@pytest.mark.gpu
+def test_replay_batch_decodes_rows():
+    """bk_replay_batch == bk_observe(states) + the packed (ids, pi, k, z), bit for bit."""
+    from blokus_rl_amd import replay
+    from blokus_rl_amd.boards import random_boards
+    from blokus_rl_amd.engine import Engine
+
+    eng = Engine(20, 4, 5)
+    states = random_boards(eng, 96, seed0=3, max_plies=40)
+    ids, counts = eng.legal_ids(states, cap=1024)
+    k = counts.clamp(min=0)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    pi = torch.rand(ids.shape, device="cuda", generator=g)
+    z = torch.randint(-1, 4, (96, 4), device="cuda").float()
+    buf, cap = replay.pack(states, ids, pi, k, z)
+    index = torch.tensor([5, 0, 95, 17, 17, 60], device="cuda")
+    out = eng.replay_batch(buf, cap, index, with_states=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out["states"], states[index])
+    assert torch.equal(out["observation"], eng.observe(states[index]))
+    assert torch.equal(out["k"], k[index])
+    assert torch.equal(out["score"], z[index])
+    w = min(cap, ids.shape[1])
+    exp_ids = torch.full((6, cap), -1, dtype=torch.int16, device="cuda")
+    exp_ids[:, :w] = ids[index][:, :w].to(torch.int16)
+    assert torch.equal(out["ids"], exp_ids)
+    exp_pi = torch.zeros((6, cap), device="cuda")
+    exp_pi[:, :w] = pi[index][:, :w]
+    assert torch.equal(out["pi"], exp_pi)
+
+
+@pytest.mark.gpu
+def test_learner_step_matches_dropin_loss():
+    """The device batch + HIP loss == the drop-in compute_loss on the reference-layout batch
+    (dense mask, padded pi): same loss, same parameter gradients."""
+    from blokus_rl_amd import replay
+    from blokus_rl_amd.alphazero.learner import DeviceReplay, Learner, alphazero_loss
+    from blokus_rl_amd.boards import random_boards
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import ResNet
+
+    eng = Engine(20, 4, 5)
+    states = random_boards(eng, 32, seed0=11, max_plies=30)
+    ids, counts = eng.legal_ids(states, cap=1024)
+    k = counts.clamp(min=0)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    pi = torch.rand(ids.shape, device="cuda", generator=g) * (torch.arange(1024, device="cuda") < k.unsqueeze(1))
+    pi = pi / pi.sum(1, keepdim=True).clamp(min=1e-9)
+    z = torch.randint(-1, 4, (32, 4), device="cuda").float()
+    buf, cap = replay.pack(states, ids, pi, k, z)
+    rb = DeviceReplay(eng, cap=1024)
+    rb.add_packed(buf, cap)
+    idx = torch.arange(32, device="cuda")
+    batch = rb.batch(idx)
+
+    torch.manual_seed(0)
+    net_a = ResNet(20, 4, eng.A, 2).cuda().train()
+    net_b = ResNet(20, 4, eng.A, 2).cuda().train()
+    net_b.load_state_dict(net_a.state_dict())
+    p, v = net_a(batch["observation"])
+    loss_a = alphazero_loss(p, v, batch)
+    loss_a.backward()
+
+    from blokus_rl_amd.neural_network import BlokusNNetWrapper
+
+    w = BlokusNNetWrapper.__new__(BlokusNNetWrapper)
+    masks, _ = eng.legal_mask(states)
+    dense = eng.unpack_mask(masks)
+    p, v = net_b(eng.observe(states))
+    kmax = int(k.max())
+    loss_b = w.compute_loss(dense, (p, v), (pi[:, :kmax], z))
+    loss_b.backward()
+    assert abs(loss_a.item() - loss_b.item()) <= 1e-5 * max(1.0, abs(loss_b.item()))
+    for (n, pa), pb in zip(net_a.named_parameters(), net_b.parameters()):
+        tol = 1e-4 * float(pb.grad.abs().max()) + 1e-7
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3, atol=tol, msg=n)
+    # and one full Learner step runs (Adam on the same device batch)
+    la = Learner(net_a, batch_size=32)
+    assert np.isfinite(la.train_step(batch).item())
+
+
+@pytest.mark.gpu
+def test_learner_epochs_on_selfplay_examples():
+    """Self-play examples -> DeviceReplay -> train_epochs: finite loss that falls on a small
+    window when it is trained repeatedly."""
+    from blokus_rl_amd.alphazero.learner import DeviceReplay, Learner
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import ResNet
+
+    eng = Engine(7, 2, 5)
+    torch.manual_seed(0)
+    net = ResNet(7, 2, eng.A, 1).cuda()
+    sp = SelfPlay(eng, net, 8, num_sims=8, seed=0)
+    sp.run(60)
+    ex = sp.examples()
+    assert ex is not None and len(ex) > 0
+    rb = DeviceReplay(eng, cap=1024)
+    rb.add_examples(ex)
+    L = Learner(net, batch_size=16)
+    first = L.train_epochs(rb, 1)
+    for _ in range(4):
+        last = L.train_epochs(rb, 1)
+    assert np.isfinite(first) and np.isfinite(last) and last < first
