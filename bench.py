@@ -302,12 +302,49 @@ def cpu_baseline_selfplay(seconds: float, model_type: str = "resnet"):
                       f"of one game from the empty board in {dt:.1f} s"}
 
 
+def bench_train(args, world, rank):
+    """§8f row 1: the learner on the device path (samples/s over all ranks; DDP over RCCL)."""
+    from blokus_rl_amd.alphazero.learner_bench import bench_learner
+    from blokus_rl_amd.engine import Engine
+
+    eng = Engine(20, 4, 5)
+    res = {}
+    for bs in (args.train_batch, 64):
+        r = bench_learner(eng, world, rank, bs, args.train_steps, 3, rows=args.train_rows,
+                          reference_steps=0 if (args.no_cpu_baseline or bs != 64) else 10,
+                          barrier=(lambda: _barrier(world)))
+        dt = _max_over_ranks(r["elapsed_s"], world)
+        r["value"] = bs * args.train_steps * world / dt
+        r["unit"] = "samples/s"
+        r["ms_per_step"] = dt / args.train_steps * 1e3
+        res[bs] = r
+    main_r = res[args.train_batch]
+    lk = main_r["loss_kernels"]
+    out = {"metric": "AlphaZero learner samples/sec (20x20 ResNet-5x64, Adam, device replay batches)",
+           "value": main_r["value"], "unit": "samples/s", "n_gpus": world, "steps": args.train_steps,
+           "ms_per_step": main_r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+           "dtype": "fp32", "data": "synthetic replay: random-play boards, Dirichlet pi, one-hot z",
+           "config": {"workload": "§8f row 1 learner", "batch_per_gpu": args.train_batch,
+                      "global_batch": args.train_batch * world, "parallelism": f"ddp{world}"},
+           "at_reference_batch_64": {k: res[64][k] for k in ("value", "unit", "ms_per_step")},
+           "roofline": {"bound": "hbm", "kernel": lk["kernel"], "achieved": lk["achieved_GBps"],
+                        "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk["achieved_GBps"] * 1e9 / HBM_PEAK,
+                        "kernel_ms": lk["ms"], "bytes_per_launch_pair": lk["bytes_per_launch_pair"],
+                        "units_per_launch": args.train_batch, "traffic": None}}
+    if "reference_path" in res[64]:
+        out["reference_path_batch_64"] = res[64]["reference_path"]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv"], default="all")
+    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train"], default="all")
+    ap.add_argument("--train-batch", type=int, default=1024)
+    ap.add_argument("--train-steps", type=int, default=20)
+    ap.add_argument("--train-rows", type=int, default=8192)
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--vec-steps", type=int, default=1000)
     ap.add_argument("--legal-steps", type=int, default=200)
@@ -328,6 +365,8 @@ def main():
         out = bench_legal(args, world, rank)
     elif args.workload == "vecenv":
         out = bench_vecenv(args, world, rank)
+    elif args.workload == "train":
+        out = bench_train(args, world, rank)
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
@@ -345,6 +384,7 @@ def main():
             vargs = argparse.Namespace(**vars(args))
             vargs.no_cpu_baseline = True
             out["ppo_vector_env"] = bench_vecenv(vargs, world, rank)
+            out["learner"] = bench_train(args, world, rank)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_selfplay(args.cpu_seconds, args.model)
             if args.workload == "all":
