@@ -118,7 +118,7 @@ class Learner:
     """Adam on the reference's net with the device batch path; DDP when a process group is up."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 1e-3, weight_decay: float = 1e-4, batch_size: int = 64,
-                 seed: int = 0, policy_fn=policy_loss, group=None):
+                 seed: int = 0, policy_fn=policy_loss, group=None, optimizer: torch.optim.Optimizer | None = None):
         self.model = model
         self.batch_size = batch_size
         self.policy_fn = policy_fn
@@ -130,7 +130,7 @@ class Learner:
             dev = next(model.parameters()).device
             self.net = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[dev.index] if dev.type == "cuda" else None, process_group=group)
-        self.optimizer = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+        self.optimizer = optimizer or torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
         self.gen = torch.Generator().manual_seed(seed)
         self.steps = 0
 

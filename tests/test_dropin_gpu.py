@@ -175,3 +175,22 @@ def test_coach_self_play_7x7():
     assert len(batched) > 0
     loss = tr._train_epochs(batched)
     assert np.isfinite(loss)
+
+
+def test_coach_device_iteration_7x7(tmp_path):
+    """One device-path iteration: batched self-play -> packed shard on disk -> replay window ->
+    learner epochs -> batched arena compare -> Elo -> checkpoint."""
+    from blokus_rl_amd import replay_io as rio
+    from blokus_rl_amd.alphazero.trainer import AlphaZeroTrainer
+
+    hp = _hp(board_size=7, number_of_players=2, model_type="resnet", num_res_blocks=1, num_mcts_sims=6,
+             games_per_gpu=6, num_eps=6, epochs=2, batch_size=32, compare_arena_games=2,
+             checkpoint_dir=str(tmp_path / "ck"), data_dir=str(tmp_path / "data"))
+    tr = AlphaZeroTrainer(hp)
+    tr.iteration = 1
+    s = tr.run_iteration_device()
+    assert s["examples"] > 0 and s["replay_rows"] == s["examples"] and np.isfinite(s["loss"])
+    assert len(s["arena_scores"]) == 2 and s["elo"] != 1000 or s["arena_scores"][0] == 0
+    shards = rio.list_shards(hp.data_dir)
+    assert len(shards) == 1 and rio.read_header(shards[0])["rows"] == s["examples"]
+    assert (tmp_path / "ck" / "checkpoint_1.pth.tar").exists()

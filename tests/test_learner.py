@@ -252,9 +252,11 @@ def test_learner_step_matches_dropin_loss():
     loss_b = w.compute_loss(dense, (p, v), (pi[:, :kmax], z))
     loss_b.backward()
     assert abs(loss_a.item() - loss_b.item()) <= 1e-5 * max(1.0, abs(loss_b.item()))
+    # one absolute scale for all tensors: the biases of convs feeding a train-mode BatchNorm have
+    # analytically zero gradients, i.e. pure rounding noise on both sides
+    scale = max(float(pb.grad.abs().max()) for pb in net_b.parameters())
     for (n, pa), pb in zip(net_a.named_parameters(), net_b.parameters()):
-        tol = 1e-4 * float(pb.grad.abs().max()) + 1e-7
-        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3, atol=tol, msg=n)
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3, atol=1e-5 * scale, msg=n)
     # and one full Learner step runs (Adam on the same device batch)
     la = Learner(net_a, batch_size=32)
     assert np.isfinite(la.train_step(batch).item())
