@@ -211,6 +211,18 @@ int bk_policy_loss_grad(const float* x, int64_t ldx, const int16_t* ids, const f
                         int cap, int B, const float* lse, float scale, const float* gscale, float* grad,
                         int64_t ldg, void* stream);
 
+/* ---------------------------------------------------------------- PPO
+ * PPOTrainer._compute_gae (ppo/trainer.py:177-211) + returns = advantages + values (:83) for a
+ * rollout of T steps x E envs ([T][E] f32, row t = step t): float32, the reference's operation
+ * order; gamma_lambda = (float)(gamma * gae_lambda) computed in double, as Python does. */
+int bk_ppo_gae(int T, int E, const float* rewards, const float* values, const float* dones, const float* next_value,
+               const float* next_done, float gamma, float gamma_lambda, float* advantages, float* returns,
+               void* stream);
+
+/* FilterLegalMoves (ppo/agent.py:27-42) from legal-move bitmasks: out = x * mask, entries equal
+ * to 0 (illegal, or a legal logit of exactly 0, as in the reference) set to -1e9. x, out [E][A]. */
+int bk_filter_legal(const float* x, int E, int A, const uint64_t* mask, int mask_words, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
