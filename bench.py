@@ -336,12 +336,52 @@ def bench_train(args, world, rank):
     return out
 
 
+def bench_ppo(args, world, rank):
+    """§8f row 4: whole PPO updates on the config-5 device env (reference config
+    ppo_blokus_7x7.yml: cnn agent, d_model 128, 32 steps per rollout; 8192 envs per GPU):
+    rollout (fused env step + device legal filter) + GAE kernel + 4 epochs of minibatch updates."""
+    from blokus_rl_amd.ppo.trainer import PPOHparams, PPOTrainer
+
+    E, T = args.envs, 32
+    hp = PPOHparams(num_envs=E, num_steps=T, agent_type="cnn", d_model=128, learning_rate=1e-5,
+                    total_timesteps=E * T * 100, seed=rank, save_interval=10**9, target_kl=None)
+    tr = PPOTrainer(hp)
+    tr.train(1)  # warm-up update
+    torch.cuda.synchronize()
+    _barrier(world)
+    t0 = time.perf_counter()
+    n = args.ppo_updates
+    tr.train(n)
+    torch.cuda.synchronize()
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    # the GAE kernel alone on this rollout
+    from blokus_rl_amd.ppo.trainer import compute_gae
+    m = tr.memory
+    nv = torch.zeros(E, device=tr.device)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    compute_gae(m.rewards, m.values, m.dones, nv, nv, 0.99, 0.95)
+    e0.record(st)
+    for _ in range(20):
+        compute_gae(m.rewards, m.values, m.dones, nv, nv, 0.99, 0.95)
+    e1.record(st)
+    torch.cuda.synchronize()
+    gae_ms = e0.elapsed_time(e1) / 20
+    gae_bytes = 5 * T * E * 4 + 2 * E * 4
+    return {"metric": "PPO env-steps/sec incl. updates (7x7 cnn agent, 32-step rollouts)",
+            "value": E * T * n * world / dt, "unit": "env-steps/s", "envs_per_gpu": E, "updates": n,
+            "s_per_update": dt / n, "last_log": {k: float(v) for k, v in tr.logs[-1].items()},
+            "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBps": gae_bytes / (gae_ms * 1e-3) / 1e9}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train"], default="all")
+    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train", "ppo"], default="all")
+    ap.add_argument("--ppo-updates", type=int, default=2)
     ap.add_argument("--train-batch", type=int, default=1024)
     ap.add_argument("--train-steps", type=int, default=20)
     ap.add_argument("--train-rows", type=int, default=8192)
@@ -367,6 +407,8 @@ def main():
         out = bench_vecenv(args, world, rank)
     elif args.workload == "train":
         out = bench_train(args, world, rank)
+    elif args.workload == "ppo":
+        out = bench_ppo(args, world, rank)
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
