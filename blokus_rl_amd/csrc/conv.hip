@@ -1,0 +1,287 @@
+// conv.hip — the leaf evaluator's 3x3 convolutions (ResNet of models/blokus_nnet.py:88-151, BN
+// folded) as one fused fp32 MFMA kernel per layer: y = act(conv3x3(x, W) + b (+ r)).
+//
+// Shape: x [B][N][N][CIN] (NHWC, the leaf batch's channels_last layout), W 64 x CIN x 3 x 3,
+// y [B][N][N][64]. As a GEMM: M = B*N*N output pixels, N = 64 channels, K = 9*CIN. At the
+// self-play batch (256 boards of 20x20, CIN = 64) that is 7.55 GFLOP per layer: MFMA-bound.
+//
+// Design (gfx950, f32-in MFMA v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD, exact f32):
+//  * One 768-thread workgroup per CU (grid 256), 12 waves = 3 per SIMD. The whole packed weight
+//    tensor sits in LDS (9*CIN*64*4 B = 147 KB at CIN=64), loaded once per launch and shared by
+//    the 8 waves; every B operand is one conflict-free ds_read_b128 (the 4 output-channel
+//    blocks of a k-step, pre-packed in MFMA lane order by the host).
+//  * A wave owns a tile of 16 consecutive output pixels x all 64 channels: 4 independent 16x16
+//    accumulators (dependent-latency 40 cycles < 4 x 32-cycle issue, so the MFMA pipe never
+//    waits on itself). Its A operand comes straight from global memory: per tap, one CIN-wide
+//    row per pixel, read VEC floats at a time (dwordx4 at CIN >= 16) in a K order permuted so
+//    each vector load feeds VEC consecutive k-steps; out-of-board taps read zeros (padding 1).
+//  * XCD-aware tiling: the 8 XCDs each take a contiguous eighth of the pixel tiles (whole boards,
+//    3.2 MB of input at B=256) so a board's rows are fetched into one XCD's L2 and reused there
+//    by all 9 taps; within an XCD the tiles are dealt round-robin over its 32 CUs, and a CU's
+//    leftover tiles are split into 16-channel quarters to even out the last round (k_conv3x3).
+//  * Epilogue fused: + bias, + residual (the tower's skip connection), ReLU, one store pass.
+// Accumulation order differs from MIOpen's (k-ordered fma chain per MFMA), so results agree
+// with the MIOpen convolution to f32 rounding, not bitwise.
+#include "../../include/blokus_engine.h"
+#include "ctx.h"
+
+#include <type_traits>
+
+namespace bk {
+namespace {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int kCout = 64;
+constexpr int kConvThreads = 768;
+constexpr int kConvWaves = kConvThreads / kWave;
+
+template <int VEC>
+struct VecT;
+template <>
+struct VecT<1> {
+  using T = float;
+  __device__ static float at(const T& v, int) { return v; }
+};
+template <>
+struct VecT<2> {
+  using T = float2;
+  __device__ static float at(const T& v, int r) { return r == 0 ? v.x : v.y; }
+};
+template <>
+struct VecT<4> {
+  using T = float4;
+  __device__ static float at(const T& v, int r) { return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w)); }
+};
+
+// A run of output tiles owned by one wave. Tile i = 16 consecutive pixels from 16*tile(i) x NJ
+// 16-channel blocks from block jblk(i), the whole K = 9*CIN reduction. k-steps per tap:
+// S = CIN / 4 (4 k values per 16x16x4 MFMA); lane group g = lane>>4 holds k index g of each
+// step; step s = q*VEC + r reads input channel cin = 4*VEC*q + VEC*g + r (the host packs W in
+// the same order).
+//
+// Software pipeline over the run's k-steps, carried across tiles (the body is fully unrolled,
+// so every ring slot is a fixed register set and the s_waitcnt counts are exact):
+//  * A: tap t's Q vector loads go to abuf[t % 3], issued at the start of tap t-2 — for taps 0
+//    and 1 of the next tile, during taps 7 and 8 of the current one, before its epilogue
+//    stores, so waiting on them never waits on the stores. Loads are unconditional (an in-board
+//    address when the tap falls off the board) and the zero padding is a multiply at use, so
+//    the compiler never sinks them into branches.
+//  * B: one LDS read per k-step (ds_read_b128 = the 4 channel blocks), DB steps ahead; the
+//    weights are the same for every tile, so the ring runs on across tile boundaries.
+template <int CIN, int VEC, bool RELU, bool RES, int NJ, class TileOf, class JblkOf>
+__device__ __forceinline__ void conv_run(const float* __restrict__ x, const f32x4* __restrict__ w_lds,
+                                         const float* __restrict__ bias, const float* __restrict__ res,
+                                         float* __restrict__ y, int N, int total_pix, int count, TileOf tile,
+                                         JblkOf jblk) {
+  constexpr int S = CIN / 4;
+  constexpr int Q = CIN / (4 * VEC);
+  constexpr int KS = 9 * S;
+  constexpr int DB = S < 8 ? S : 8;  // B prefetch distance in k-steps (divides KS)
+  static_assert(KS % DB == 0, "ring must wrap at tile boundaries");
+  using V = typename VecT<VEC>::T;
+  using WT = typename std::conditional<NJ == 4, f32x4, float>::type;
+  if (count <= 0) return;
+  const int l = threadIdx.x & 63;
+  const int m = l & 15, g = l >> 4;
+  const int npix = N * N;
+  struct Pix {
+    int b, py, px;
+    bool in;
+  };
+  auto pix_of = [&](int t) {
+    Pix q;
+    const int p = t * 16 + m;
+    q.in = p < total_pix;
+    q.b = q.in ? p / npix : 0;
+    const int rem = p - q.b * npix;
+    q.py = rem / N;
+    q.px = rem - q.py * N;
+    return q;
+  };
+  V abuf[3][Q];
+  float keep[3];
+  auto load_tap = [&](const Pix& pp, int tap, V* dst, float& kp) {
+    const int yy = pp.py + tap / 3 - 1, xx = pp.px + tap % 3 - 1;
+    const bool ok = pp.in && yy >= 0 && yy < N && xx >= 0 && xx < N;
+    const int yc = ok ? yy : pp.py, xc = ok ? xx : pp.px;
+    const float* src = x + ((int64_t)(pp.b * N + yc) * N + xc) * CIN + VEC * g;
+    kp = ok ? 1.0f : 0.0f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      dst[q] = *reinterpret_cast<const V*>(src + 4 * VEC * q);
+    }
+  };
+  int j0 = jblk(0);
+  auto read_w = [&](int ks) -> WT {
+    if constexpr (NJ == 4) {
+      return w_lds[ks * kWave + l];
+    } else {
+      return reinterpret_cast<const float*>(w_lds + ks * kWave + l)[j0];
+    }
+  };
+  float bias_r[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bias_r[j] = bias[16 * (j0 + j) + m];
+  Pix cur = pix_of(tile(0));
+  WT wring[DB];
+  load_tap(cur, 0, abuf[0], keep[0]);
+  load_tap(cur, 1, abuf[1], keep[1]);
+#pragma unroll
+  for (int s = 0; s < DB; ++s) wring[s] = read_w(s);
+  for (int i = 0; i < count; ++i) {
+    const int t = tile(i);
+    const bool more = i + 1 < count;
+    const Pix nxt = pix_of(more ? tile(i + 1) : t);
+    f32x4 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+      for (int sl = 0; sl < S; ++sl) {
+        const int ks = tap * S + sl;
+        if (sl == 0) {
+          if (tap + 2 < 9) load_tap(cur, tap + 2, abuf[(tap + 2) % 3], keep[(tap + 2) % 3]);
+          else if (more) load_tap(nxt, tap + 2 - 9, abuf[(tap + 2) % 3], keep[(tap + 2) % 3]);
+        }
+        const WT w = wring[ks % DB];
+        wring[ks % DB] = read_w((ks + DB) % KS);
+        const float av = VecT<VEC>::at(abuf[tap % 3][sl / VEC], sl % VEC) * keep[tap % 3];
+        if constexpr (NJ == 4) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w[0], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w[1], acc[1], 0, 0, 0);
+          acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w[2], acc[2], 0, 0, 0);
+          acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w[3], acc[3], 0, 0, 0);
+        } else {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w, acc[0], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // D layout: lane l holds rows (pixels) 4g + v, column (channel) m of each 16x16 block
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int po = t * 16 + 4 * g + v;
+      if (po < total_pix) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const size_t o = (size_t)po * kCout + 16 * (j0 + j) + m;
+          float val = acc[j][v] + bias_r[j];
+          if (RES) val = val + res[o];
+          if (RELU) val = fmaxf(val, 0.0f);
+          y[o] = val;
+        }
+      }
+    }
+    cur = nxt;
+    if constexpr (NJ == 1) {  // quarter tiles may change channel block: refresh B ring + bias
+      if (more && jblk(i + 1) != j0) {
+        j0 = jblk(i + 1);
+        bias_r[0] = bias[16 * j0 + m];
+#pragma unroll
+        for (int s = 0; s < DB; ++s) wring[s] = read_w(s);
+      }
+    }
+  }
+}
+
+// Work split: the 8 XCDs take contiguous eighths of the 16-pixel tiles; inside an XCD, tile
+// i of CU c is global tile t_begin + c + ncu*i. A CU's waves take whole tiles round-robin for
+// R = floor(T_cu / waves) rounds; the L < waves leftover tiles are cut into 4L quarter tiles
+// (16 channels each) dealt over the waves, so no SIMD carries a whole extra tile at the end.
+template <int CIN, int VEC, bool RELU, bool RES>
+__global__ __launch_bounds__(kConvThreads) void k_conv3x3(const float* __restrict__ x, const f32x4* __restrict__ wp,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ res, float* __restrict__ y,
+                                                          int N, int total_pix) {
+  constexpr int S = CIN / 4;
+  extern __shared__ __attribute__((aligned(16))) f32x4 w_lds[];  // [9][S][64 lanes] x (4 channel blocks)
+  const int tiles = (total_pix + 15) >> 4;
+  const int nxcd = 8;
+  const int xcd = blockIdx.x % nxcd, cu = blockIdx.x / nxcd, ncu = gridDim.x / nxcd;
+  const int t_begin = (int)((int64_t)tiles * xcd / nxcd), t_end = (int)((int64_t)tiles * (xcd + 1) / nxcd);
+  if (t_begin + cu >= t_end) return;  // block-uniform: nothing to do here
+  for (int i = threadIdx.x; i < 9 * S * kWave; i += kConvThreads) w_lds[i] = wp[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  const int t_cu = (t_end - t_begin - cu + ncu - 1) / ncu;  // tiles of this CU
+  const int rounds = t_cu / kConvWaves;
+  const int left = t_cu - rounds * kConvWaves;
+  const int base = t_begin + cu;
+  conv_run<CIN, VEC, RELU, RES, 4>(
+      x, w_lds, bias, res, y, N, total_pix, rounds, [&](int r) { return base + ncu * (r * kConvWaves + wave); },
+      [](int) { return 0; });
+  const int nq = wave < 4 * left ? (4 * left - wave + kConvWaves - 1) / kConvWaves : 0;
+  conv_run<CIN, VEC, RELU, RES, 1>(
+      x, w_lds, bias, res, y, N, total_pix, nq,
+      [&](int i) { return base + ncu * (rounds * kConvWaves + (wave + i * kConvWaves) / 4); },
+      [&](int i) { return (wave + i * kConvWaves) % 4; });
+}
+
+template <int CIN, int VEC>
+int launch_conv(const float* x, const f32x4* wp, const float* b, const float* r, float* y, int N, int total,
+                int relu, hipStream_t s, int blocks) {
+  const size_t lds = sizeof(f32x4) * 9 * (CIN / 4) * kWave;
+  if (relu && r)
+    hipLaunchKernelGGL((k_conv3x3<CIN, VEC, true, true>), dim3(blocks), dim3(kConvThreads), lds, s, x, wp, b, r, y, N,
+                       total);
+  else if (relu)
+    hipLaunchKernelGGL((k_conv3x3<CIN, VEC, true, false>), dim3(blocks), dim3(kConvThreads), lds, s, x, wp, b, r, y,
+                       N, total);
+  else if (r)
+    hipLaunchKernelGGL((k_conv3x3<CIN, VEC, false, true>), dim3(blocks), dim3(kConvThreads), lds, s, x, wp, b, r, y,
+                       N, total);
+  else
+    hipLaunchKernelGGL((k_conv3x3<CIN, VEC, false, false>), dim3(blocks), dim3(kConvThreads), lds, s, x, wp, b, r, y,
+                       N, total);
+  return launch_check("k_conv3x3");
+}
+
+}  // namespace
+}  // namespace bk
+
+using namespace bk;
+
+extern "C" {
+
+int bk_conv3x3_packed_floats(int cin) { return (cin == 4 || cin == 8 || cin == 64) ? 9 * cin * kCout : -1; }
+
+int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, const float* bias, const float* residual,
+               int relu, float* y, void* stream) {
+  BK_REQUIRE(x && wpacked && bias && y && B >= 0 && N > 0 && N <= 32, "bad argument");
+  BK_REQUIRE(cin == 4 || cin == 8 || cin == 64, "bk_conv3x3: cin must be 4, 8 or 64");
+  BK_REQUIRE(((uintptr_t)x & 15u) == 0 && ((uintptr_t)wpacked & 15u) == 0, "bk_conv3x3: 16-byte aligned x, weights");
+  if (B == 0) return BK_OK;
+  const int64_t total = (int64_t)B * N * N;
+  BK_REQUIRE(total < (1ll << 30), "bk_conv3x3: batch too large");
+  static int blocks = 0;
+  if (!blocks) {
+    int dev = 0, cus = 256;
+    if (hip_check(hipGetDevice(&dev), "hipGetDevice") != BK_OK) return BK_EHIP;
+    if (hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute") !=
+        BK_OK)
+      return BK_EHIP;
+    blocks = (cus / 8) * 8 > 0 ? (cus / 8) * 8 : 8;
+  }
+  const f32x4* wp = reinterpret_cast<const f32x4*>(wpacked);
+  hipStream_t s = (hipStream_t)stream;
+  if (cin == 64) {
+    static bool attr_set = false;
+    if (!attr_set) {  // 147 KB of dynamic LDS (above the 64 KB default)
+      const int bytes = (int)(sizeof(f32x4) * 9 * 16 * kWave);
+      const void* fns[4] = {(const void*)k_conv3x3<64, 4, true, true>, (const void*)k_conv3x3<64, 4, true, false>,
+                            (const void*)k_conv3x3<64, 4, false, true>, (const void*)k_conv3x3<64, 4, false, false>};
+      for (const void* fn : fns)
+        if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes),
+                      "hipFuncSetAttribute") != BK_OK)
+          return BK_EHIP;
+      attr_set = true;
+    }
+    return launch_conv<64, 4>(x, wp, bias, residual, y, N, (int)total, relu, s, blocks);
+  }
+  if (cin == 8) return launch_conv<8, 2>(x, wp, bias, residual, y, N, (int)total, relu, s, blocks);
+  return launch_conv<4, 1>(x, wp, bias, residual, y, N, (int)total, relu, s, blocks);
+}
+
+}  // extern "C"

@@ -59,6 +59,9 @@ _SIGS = {
                                  ctypes.c_int64, _vp]),
     "bk_ppo_gae": (_i, [_i, _i, _vp, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp]),
     "bk_filter_legal": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp]),
+    "bk_bias_act": (_i, [_vp, ctypes.c_int64, _i, _vp, _vp, _i, _vp]),
+    "bk_conv3x3_packed_floats": (_i, [_i]),
+    "bk_conv3x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),
 }
 
 _LIB = None

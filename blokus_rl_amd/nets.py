@@ -11,6 +11,8 @@ semantics and `state_dict` keys follow the reference so its checkpoints load unc
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -152,8 +154,101 @@ class FusedResNet(nn.Module):
         return p, v
 
 
+def _bias_act(x: torch.Tensor, bias: torch.Tensor, relu: bool, residual: torch.Tensor | None = None):
+    """In-place x = act(x + bias (+ residual)) on a channels_last activation (bk_bias_act)."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    assert x.is_contiguous(memory_format=torch.channels_last) and x.dtype == torch.float32
+    if residual is not None:
+        assert residual.is_contiguous(memory_format=torch.channels_last) and residual.shape == x.shape
+    _check(load_library().bk_bias_act(ctypes.c_void_p(x.data_ptr()), x.numel(), x.shape[1], _ptr(bias),
+                                      None if residual is None else ctypes.c_void_p(residual.data_ptr()),
+                                      int(relu), _stream(x.device)))
+    return x
+
+
+def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
+    """[64, cin, 3, 3] weights -> bk_conv3x3's operand order: flat [9][cin/4][64 lanes][4 blocks],
+    element (tap, s, l, j) = w[16j + (l & 15), cin(s, l >> 4), tap // 3, tap % 3] with
+    cin(s, g) = 4*VEC*(s // VEC) + VEC*g + s % VEC, VEC = 4 (cin % 16 == 0), 2 (cin 8), 1 (cin 4)."""
+    cout, cin = w.shape[0], w.shape[1]
+    assert cout == 64 and w.shape[2:] == (3, 3) and cin in (4, 8, 64)
+    vec = 4 if cin % 16 == 0 else (2 if cin == 8 else 1)
+    dev = w.device
+    tap = torch.arange(9, device=dev).view(9, 1, 1, 1)
+    s = torch.arange(cin // 4, device=dev).view(1, -1, 1, 1)
+    lane = torch.arange(64, device=dev).view(1, 1, 64, 1)
+    j = torch.arange(4, device=dev).view(1, 1, 1, 4)
+    ci = 4 * vec * (s // vec) + vec * (lane >> 4) + s % vec
+    co = 16 * j + (lane & 15)
+    out = w.float()[co, ci, tap // 3, tap % 3]
+    return out.contiguous().view(-1)
+
+
+def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bool,
+            residual: torch.Tensor | None = None) -> torch.Tensor:
+    """bk_conv3x3 on a channels_last activation [B, cin, N, N] -> [B, 64, N, N] channels_last."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, cin, N, _ = x.shape
+    assert x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+    y = torch.empty((B, 64, N, N), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    if residual is not None:
+        assert residual.is_contiguous(memory_format=torch.channels_last) and residual.shape == y.shape
+    _check(load_library().bk_conv3x3(ctypes.c_void_p(x.data_ptr()), B, N, cin, _ptr(wpacked), _ptr(bias),
+                                     None if residual is None else ctypes.c_void_p(residual.data_ptr()), int(relu),
+                                     ctypes.c_void_p(y.data_ptr()), _stream(x.device)))
+    return y
+
+
+class LeafResNet(nn.Module):
+    """The leaf evaluator's ResNet on the device (fp32, channels_last): FusedResNet's function
+    with every 3x3 conv + bias + ReLU (+ the tower's residual) as one bk_conv3x3 launch (fp32
+    MFMA, weights resident in LDS); the 1x1 heads run bias-free in MIOpen with a bk_bias_act
+    epilogue; the policy/value linears and log-softmax stay in PyTorch."""
+
+    def __init__(self, net: ResNet):
+        super().__init__()
+        self.f = FusedResNet(net).eval()
+        f = self.f
+        self.native = f.stem.out_channels == 64 and f.stem.in_channels in (4, 8, 64)
+        if self.native:
+            self.register_buffer("w_stem", pack_conv3x3(f.stem.weight.detach()))
+            for i, (c1, c2) in enumerate(f.blocks):
+                self.register_buffer(f"w_{i}_1", pack_conv3x3(c1.weight.detach()))
+                self.register_buffer(f"w_{i}_2", pack_conv3x3(c2.weight.detach()))
+
+    @torch.no_grad()
+    def forward(self, x):
+        f = self.f
+        x = x.float().contiguous(memory_format=torch.channels_last)
+        n = len(f.blocks)
+        if self.native:
+            x = conv3x3(x, self.w_stem, f.stem.bias, True)
+            h = x
+            for i, (c1, c2) in enumerate(f.blocks):
+                h = conv3x3(h, getattr(self, f"w_{i}_1"), c1.bias, True)
+                h = conv3x3(h, getattr(self, f"w_{i}_2"), c2.bias, i + 1 == n, x if i + 1 == n else None)
+        else:
+            conv = lambda t, c: F.conv2d(t, c.weight, None, c.stride, c.padding)  # noqa: E731
+            x = _bias_act(conv(x, f.stem), f.stem.bias, True)
+            h = x
+            for i, (c1, c2) in enumerate(f.blocks):
+                h = _bias_act(conv(h, c1), c1.bias, True)
+                h = _bias_act(conv(h, c2), c2.bias, i + 1 == n, x if i + 1 == n else None)
+        x = h if n else F.relu(x + x)
+        conv1 = lambda t, c: F.conv2d(t, c.weight, None).contiguous(memory_format=torch.channels_last)  # noqa: E731
+        p = _bias_act(conv1(x, f.policy_conv), f.policy_conv.bias, True)
+        p = F.log_softmax(f.policy_out(p.contiguous().flatten(1)), dim=1)
+        v = _bias_act(conv1(x, f.value_conv), f.value_conv.bias, True)
+        v = torch.tanh(f.value_fc2(F.relu(f.value_fc1(v.contiguous().flatten(1)))))
+        return p, v
+
+
 def inference_model(model: nn.Module) -> nn.Module:
-    """The leaf evaluator's form of a net (BN folded for ResNet, eval otherwise)."""
+    """The leaf evaluator's form of a net: ResNet -> LeafResNet on a HIP device (FusedResNet
+    elsewhere), eval() otherwise."""
     if isinstance(model, ResNet):
-        return FusedResNet(model).eval()
+        dev = next(model.parameters()).device
+        return (LeafResNet(model) if dev.type == "cuda" else FusedResNet(model)).eval()
     return model.eval()

@@ -223,6 +223,21 @@ int bk_ppo_gae(int T, int E, const float* rewards, const float* values, const fl
  * to 0 (illegal, or a legal logit of exactly 0, as in the reference) set to -1e9. x, out [E][A]. */
 int bk_filter_legal(const float* x, int E, int A, const uint64_t* mask, int mask_words, float* out, void* stream);
 
+/* ---------------------------------------------------------------- leaf-evaluator epilogue
+ * The conv epilogues of the inference ResNet (models/blokus_nnet.py:135-151, BN folded):
+ * in place on x[n] (NHWC, C channels innermost): x = act(x + bias[c] (+ residual)), act = ReLU
+ * when relu != 0. residual may be NULL. */
+int bk_bias_act(float* x, int64_t n, int C, const float* bias, const float* residual, int relu, void* stream);
+
+/* 3x3 convolution, stride 1, zero padding 1, 64 output channels, with the fused epilogue
+ * y = act(conv(x) + bias (+ residual)): x [B][N][N][cin] and y, residual [B][N][N][64] NHWC f32,
+ * cin in {4, 8, 64}. wpacked: the 9*cin*64 weights in the kernel's MFMA operand order
+ * (blokus_rl_amd/nets.py pack_conv3x3 documents it); bk_conv3x3_packed_floats(cin) = its length.
+ * Replaces conv + BN (folded) + ReLU (+ residual add) of blokus_nnet.py:135-146. */
+int bk_conv3x3_packed_floats(int cin);
+int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, const float* bias, const float* residual,
+               int relu, float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,61 @@
+"""bk_conv3x3 (fp32 MFMA 3x3 conv with fused bias / residual / ReLU) against torch's fp32
+convolution (the "plain PyTorch fp32 reference of the same op"), and LeafResNet against the
+reference-layout ResNet. Tolerance: the MFMA kernel sums K = 9*cin products in a different order
+than MIOpen, so agreement is to f32 rounding: |diff| <= 1e-5 * (sum_k |x_k w_k| + 1) per output."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, b, relu, res):
+    y = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    if res is not None:
+        y = y + res.double()
+    if relu:
+        y = torch.relu(y)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), None, padding=1) + 1.0
+    return y, bound
+
+
+@pytest.mark.parametrize("B,N,cin", [(256, 20, 64), (3, 20, 64), (1, 20, 8), (256, 20, 8), (5, 7, 4), (7, 7, 64),
+                                     (33, 20, 64)])
+@pytest.mark.parametrize("relu,use_res", [(True, False), (False, False), (True, True), (False, True)])
+def test_conv3x3_matches_torch(B, N, cin, relu, use_res):
+    from blokus_rl_amd.nets import conv3x3, pack_conv3x3
+
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N * 10 + cin)
+    x = torch.randn((B, cin, N, N), device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    w = torch.randn((64, cin, 3, 3), device="cuda", generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(64, device="cuda", generator=g) * 0.1
+    res = (torch.randn((B, 64, N, N), device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+           if use_res else None)
+    y = conv3x3(x, pack_conv3x3(w), b, relu, res)
+    torch.cuda.synchronize()
+    ref, bound = _ref(x, w, b, relu, res)
+    err = (y.double() - ref).abs()
+    assert bool((err <= 1e-5 * bound).all()), float((err / bound).max())
+    assert y.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_leaf_resnet_matches_reference_forward():
+    from blokus_rl_amd.nets import LeafResNet, ResNet
+
+    torch.manual_seed(0)
+    for N, P, A in ((20, 4, 30433), (7, 2, 2522)):
+        net = ResNet(N, P, A, 3).cuda().eval()
+        with torch.no_grad():
+            for m in net.modules():
+                if isinstance(m, torch.nn.BatchNorm2d):
+                    m.running_mean.uniform_(-0.2, 0.2)
+                    m.running_var.uniform_(0.5, 1.5)
+        leaf = LeafResNet(net).eval()
+        assert leaf.native
+        x = (torch.rand(64, 2 * P, N, N, device="cuda") < 0.3).float()
+        with torch.no_grad():
+            lp_ref, v_ref = net(x)
+            lp, v = leaf(x)
+        assert (lp - lp_ref).abs().max().item() < 2e-4
+        assert (lp.exp() - lp_ref.exp()).abs().max().item() < 1e-6
+        assert (v - v_ref).abs().max().item() < 1e-5

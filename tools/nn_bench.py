@@ -3,7 +3,7 @@ max deviation of p/v from the fp32 eval-mode ResNet. Run on a GPU box."""
 import sys, os, time, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
-from blokus_rl_amd.nets import ResNet, FusedResNet
+from blokus_rl_amd.nets import ResNet, FusedResNet, LeafResNet
 
 torch.manual_seed(0)
 dev = "cuda"
@@ -60,6 +60,8 @@ run("resnet_fp32_eager", net, graph=False)
 run("resnet_fp32_graph", net)
 fused = FusedResNet(net).eval()
 run("fused_fp32", fused)
+run("leaf_fp32_cl", LeafResNet(net).eval(), None, cl=True)
+run("leaf_fp32_cl_graph", LeafResNet(net).eval(), None, cl=True, graph=True)
 torch.backends.cudnn.benchmark = True
 run("fused_fp32_bench", fused)
 run("fused_fp16", fused, torch.float16)
