@@ -63,7 +63,8 @@ class LeafEvaluator:
             self.model = None
             return
         from ..nets import inference_model
-        self.model = inference_model(model).to(memory_format=torch.channels_last)
+        # raw policy logits are enough: k_expand_backup takes the softmax over the legal ids
+        self.model = inference_model(model, normalize=False, dtype=dtype).to(memory_format=torch.channels_last)
         self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32,
                                       device=dev).contiguous(memory_format=torch.channels_last)
         self.graph = None

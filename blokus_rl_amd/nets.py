@@ -201,15 +201,37 @@ def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bo
     return y
 
 
+def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
+    """bk_resnet_heads: tower output [B, 64, N, N] channels_last -> (policy features [B, 2*N*N] in
+    the NCHW flatten order, values [B, P])."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, C, N, _ = x.shape
+    assert C == 64 and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+    P = f.value_fc2.out_features
+    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=x.device)
+    v = torch.empty((B, P), dtype=torch.float32, device=x.device)
+    c = lambda t: t.detach().float().contiguous()  # noqa: E731
+    wp, wv = c(f.policy_conv.weight.view(2, 64)), c(f.value_conv.weight.view(64))
+    _check(load_library().bk_resnet_heads(ctypes.c_void_p(x.data_ptr()), B, N * N, _ptr(wp), _ptr(c(f.policy_conv.bias)),
+                                          _ptr(wv), _ptr(c(f.value_conv.bias)), _ptr(c(f.value_fc1.weight)),
+                                          _ptr(c(f.value_fc1.bias)), _ptr(c(f.value_fc2.weight)),
+                                          _ptr(c(f.value_fc2.bias)), P, _ptr(pf), _ptr(v), _stream(x.device)))
+    return pf, v
+
+
 class LeafResNet(nn.Module):
     """The leaf evaluator's ResNet on the device (fp32, channels_last): FusedResNet's function
     with every 3x3 conv + bias + ReLU (+ the tower's residual) as one bk_conv3x3 launch (fp32
-    MFMA, weights resident in LDS); the 1x1 heads run bias-free in MIOpen with a bk_bias_act
-    epilogue; the policy/value linears and log-softmax stay in PyTorch."""
+    MFMA, weights resident in LDS), both heads' 1x1 convs and the whole value MLP in one
+    bk_resnet_heads launch, and the policy Linear in hipBLASLt. With normalize=False the policy
+    comes back as raw logits (the leaf batch's consumer, k_expand_backup, takes a softmax over the
+    legal ids, which a per-row shift does not change), skipping the full-row log-softmax."""
 
-    def __init__(self, net: ResNet):
+    def __init__(self, net: ResNet, normalize: bool = True):
         super().__init__()
         self.f = FusedResNet(net).eval()
+        self.normalize = normalize
         f = self.f
         self.native = f.stem.out_channels == 64 and f.stem.in_channels in (4, 8, 64)
         if self.native:
@@ -237,18 +259,25 @@ class LeafResNet(nn.Module):
                 h = _bias_act(conv(h, c1), c1.bias, True)
                 h = _bias_act(conv(h, c2), c2.bias, i + 1 == n, x if i + 1 == n else None)
         x = h if n else F.relu(x + x)
-        conv1 = lambda t, c: F.conv2d(t, c.weight, None).contiguous(memory_format=torch.channels_last)  # noqa: E731
-        p = _bias_act(conv1(x, f.policy_conv), f.policy_conv.bias, True)
-        p = F.log_softmax(f.policy_out(p.contiguous().flatten(1)), dim=1)
-        v = _bias_act(conv1(x, f.value_conv), f.value_conv.bias, True)
-        v = torch.tanh(f.value_fc2(F.relu(f.value_fc1(v.contiguous().flatten(1)))))
-        return p, v
+        if self.native:
+            pf, v = resnet_heads(x, f)
+            logits = f.policy_out(pf)
+        else:
+            conv1 = lambda t, c: F.conv2d(t, c.weight, None).contiguous(memory_format=torch.channels_last)  # noqa: E731
+            p = _bias_act(conv1(x, f.policy_conv), f.policy_conv.bias, True)
+            logits = f.policy_out(p.contiguous().flatten(1))
+            v = _bias_act(conv1(x, f.value_conv), f.value_conv.bias, True)
+            v = torch.tanh(f.value_fc2(F.relu(f.value_fc1(v.contiguous().flatten(1)))))
+        return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
 
 
-def inference_model(model: nn.Module) -> nn.Module:
-    """The leaf evaluator's form of a net: ResNet -> LeafResNet on a HIP device (FusedResNet
-    elsewhere), eval() otherwise."""
+def inference_model(model: nn.Module, normalize: bool = True, dtype: torch.dtype = torch.float32) -> nn.Module:
+    """The leaf evaluator's form of a net: ResNet -> LeafResNet (fp32 HIP kernels) on a HIP
+    device, FusedResNet for reduced-precision autocast runs or off the device; eval() otherwise.
+    normalize=False lets LeafResNet return raw policy logits (see LeafResNet)."""
     if isinstance(model, ResNet):
         dev = next(model.parameters()).device
-        return (LeafResNet(model) if dev.type == "cuda" else FusedResNet(model)).eval()
+        if dev.type == "cuda" and dtype == torch.float32:
+            return LeafResNet(model, normalize=normalize).eval()
+        return FusedResNet(model).eval()
     return model.eval()

@@ -59,3 +59,33 @@ def test_leaf_resnet_matches_reference_forward():
         assert (lp - lp_ref).abs().max().item() < 2e-4
         assert (lp.exp() - lp_ref.exp()).abs().max().item() < 1e-6
         assert (v - v_ref).abs().max().item() < 1e-5
+
+
+def test_resnet_heads_kernel_matches_torch():
+    from blokus_rl_amd.nets import FusedResNet, ResNet, resnet_heads
+
+    torch.manual_seed(1)
+    for N, P, A in ((20, 4, 30433), (7, 2, 2522)):
+        f = FusedResNet(ResNet(N, P, A, 1).cuda().eval()).eval()
+        x = torch.relu(torch.randn(37, 64, N, N, device="cuda")).contiguous(memory_format=torch.channels_last)
+        pf, v = resnet_heads(x, f)
+        with torch.no_grad():
+            p_ref = torch.relu(f.policy_conv(x)).contiguous().flatten(1)
+            v_ref = torch.tanh(f.value_fc2(torch.relu(f.value_fc1(torch.relu(f.value_conv(x)).contiguous().flatten(1)))))
+        assert (pf - p_ref).abs().max().item() < 1e-5 * max(1.0, p_ref.abs().max().item())
+        assert (v - v_ref).abs().max().item() < 1e-5
+
+
+def test_leaf_resnet_raw_logits_give_same_masked_softmax():
+    from blokus_rl_amd.nets import LeafResNet, ResNet
+
+    torch.manual_seed(2)
+    net = ResNet(20, 4, 30433, 2).cuda().eval()
+    x = (torch.rand(8, 8, 20, 20, device="cuda") < 0.3).float()
+    lp, v = LeafResNet(net).eval()(x)
+    lg, v2 = LeafResNet(net, normalize=False).eval()(x)
+    assert torch.equal(v, v2)
+    ids = torch.randperm(30433, device="cuda")[:300]
+    a = torch.softmax(lp[:, ids], 1)
+    b = torch.softmax(lg[:, ids], 1)
+    assert (a - b).abs().max().item() < 1e-6
