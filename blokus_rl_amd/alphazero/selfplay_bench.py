@@ -78,6 +78,30 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     return sp, eng, done, elapsed, delta, ms
 
 
+def time_leaf_conv(sp, reps: int = 20):
+    """The dominant kernel of the self-play step, k_conv3x3 (a residual-block conv of the leaf
+    evaluator, 64 -> 64 channels at the leaf batch), timed live with HIP events on the stream it
+    is launched on. -> (ms per launch, algorithmic FLOP per launch) or None (no ResNet)."""
+    from ..nets import LeafResNet, conv3x3
+
+    model = getattr(sp.evaluator, "model", None)
+    if not isinstance(model, LeafResNet) or not model.native or not len(model.f.blocks):
+        return None
+    G, N = sp.G, sp.eng.N
+    x = torch.relu(torch.randn((G, 64, N, N), device=sp.eng.device)).contiguous(memory_format=torch.channels_last)
+    w, b = model.w_0_1, model.f.blocks[0][0].bias
+    for _ in range(3):
+        conv3x3(x, w, b, True)
+    st = torch.cuda.current_stream(sp.eng.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        conv3x3(x, w, b, True)
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, 2.0 * G * N * N * 64 * 9 * 64
+
+
 def bench_selfplay(args, world, rank):
     G = args.games
     sp, eng, sims, elapsed, delta, ms = run_selfplay(args.model, args.nn_dtype, G, args.sims, args.steps,
@@ -96,6 +120,7 @@ def bench_selfplay(args, world, rank):
     achieved = sbytes / steps_sim / (search_ms * 1e-3) if search_ms else 0.0
     net_flops = RESNET_FLOPS_PER_LEAF * delta["expanded"] / steps_sim
     net_peak = FP32_PEAK if args.nn_dtype == "fp32" else FP16_PEAK
+    conv = time_leaf_conv(sp) if args.nn_dtype == "fp32" else None
     out = {
         "metric": "MCTS sims/sec on 20x20 Blokus (4 players, 256 games/GPU, 100 sims/move)",
         "value": sims / elapsed,
@@ -112,15 +137,25 @@ def bench_selfplay(args, world, rank):
         "config": {"workload": "config 3 (N=1) / 4 (N=8): AlphaZero self-play 20x20, 256 concurrent games per GPU, "
                                "100 sims/move, ResNet-5x64 leaf eval", "global_batch": G * world,
                    "parallelism": f"dp{world} (independent games)", "model": args.model},
-        "roofline": {"bound": "hbm", "kernel": "k_select+k_expand_backup (search)",
-                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": None,
-                     "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms},
-        "net_roofline": {"bound": "mfma", "kernel": "ResNet forward (MIOpen/hipBLASLt, BN folded)",
+        "search_roofline": {"bound": "hbm", "kernel": "k_select+k_expand_backup (search)",
+                            "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK, "traffic": None,
+                            "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms},
+        "net_roofline": {"bound": "mfma",
+                         "kernel": "leaf ResNet forward (k_conv3x3 x 11, k_resnet_heads, hipBLASLt policy Linear)",
                          "achieved": net_flops / (ms.get("net", 1e9) * 1e-3) / 1e12 if ms else None,
                          "peak": net_peak / 1e12, "unit": "TFLOP/s",
                          "frac": (net_flops / (ms["net"] * 1e-3)) / net_peak if ms else None},
         "stage_ms_per_sim_step": ms,
         "engine_counters": delta,
     }
+    if conv is not None:
+        cms, cflop = conv
+        out["roofline"] = {"bound": "mfma", "kernel": "k_conv3x3 (64->64, 3x3, fused bias+ReLU)",
+                           "achieved": cflop / (cms * 1e-3) / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
+                           "frac": cflop / (cms * 1e-3) / FP32_PEAK, "traffic": None, "kernel_ms": cms,
+                           "flop_per_launch": cflop, "units_per_launch": G,
+                           "launches_per_sim_step": 10, "share_of_sim_step": 10 * cms / (elapsed / steps_sim * 1e3)}
+    else:
+        out["roofline"] = out["search_roofline"]
     return out

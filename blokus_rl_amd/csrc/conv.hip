@@ -17,7 +17,8 @@
 //    each vector load feeds VEC consecutive k-steps; out-of-board taps read zeros (padding 1).
 //  * XCD-aware tiling: the 8 XCDs each take a contiguous eighth of the pixel tiles (whole boards,
 //    3.2 MB of input at B=256) so a board's rows are fetched into one XCD's L2 and reused there
-//    by all 9 taps; within an XCD the tiles are dealt round-robin over its 32 CUs, and a CU's
+//    by all 9 taps; within an XCD each CU takes a contiguous run of tiles (its waves share board
+//    rows in L1), and a CU's
 //    leftover tiles are split into 16-channel quarters to even out the last round (k_conv3x3).
 //  * Epilogue fused: + bias, + residual (the tower's skip connection), ReLU, one store pass.
 // Accumulation order differs from MIOpen's (k-ordered fma chain per MFMA), so results agree
@@ -186,8 +187,8 @@ __device__ __forceinline__ void conv_run(const float* __restrict__ x, const f32x
   }
 }
 
-// Work split: the 8 XCDs take contiguous eighths of the 16-pixel tiles; inside an XCD, tile
-// i of CU c is global tile t_begin + c + ncu*i. A CU's waves take whole tiles round-robin for
+// Work split: the 8 XCDs take contiguous eighths of the 16-pixel tiles; inside an XCD, each CU
+// takes a contiguous run of them. A CU's waves take whole tiles round-robin for
 // R = floor(T_cu / waves) rounds; the L < waves leftover tiles are cut into 4L quarter tiles
 // (16 channels each) dealt over the waves, so no SIMD carries a whole extra tile at the end.
 template <int CIN, int VEC, bool RELU, bool RES>
@@ -201,21 +202,25 @@ __global__ __launch_bounds__(kConvThreads) void k_conv3x3(const float* __restric
   const int nxcd = 8;
   const int xcd = blockIdx.x % nxcd, cu = blockIdx.x / nxcd, ncu = gridDim.x / nxcd;
   const int t_begin = (int)((int64_t)tiles * xcd / nxcd), t_end = (int)((int64_t)tiles * (xcd + 1) / nxcd);
-  if (t_begin + cu >= t_end) return;  // block-uniform: nothing to do here
+  if ((int64_t)(t_end - t_begin) * (cu + 1) / ncu == (int64_t)(t_end - t_begin) * cu / ncu) return;  // no tiles here
   for (int i = threadIdx.x; i < 9 * S * kWave; i += kConvThreads) w_lds[i] = wp[i];
   __syncthreads();
   const int wave = threadIdx.x >> 6;
-  const int t_cu = (t_end - t_begin - cu + ncu - 1) / ncu;  // tiles of this CU
+  // contiguous tiles per CU: its waves work on neighbouring 16-pixel strips at the same time,
+  // so the board rows their 9 taps read are shared in the CU's L1
+  const int range = t_end - t_begin;
+  const int c_lo = (int)((int64_t)range * cu / ncu), c_hi = (int)((int64_t)range * (cu + 1) / ncu);
+  const int t_cu = c_hi - c_lo;
   const int rounds = t_cu / kConvWaves;
   const int left = t_cu - rounds * kConvWaves;
-  const int base = t_begin + cu;
+  const int base = t_begin + c_lo;
   conv_run<CIN, VEC, RELU, RES, 4>(
-      x, w_lds, bias, res, y, N, total_pix, rounds, [&](int r) { return base + ncu * (r * kConvWaves + wave); },
+      x, w_lds, bias, res, y, N, total_pix, rounds, [&](int r) { return base + r * kConvWaves + wave; },
       [](int) { return 0; });
   const int nq = wave < 4 * left ? (4 * left - wave + kConvWaves - 1) / kConvWaves : 0;
   conv_run<CIN, VEC, RELU, RES, 1>(
       x, w_lds, bias, res, y, N, total_pix, nq,
-      [&](int i) { return base + ncu * (rounds * kConvWaves + (wave + i * kConvWaves) / 4); },
+      [&](int i) { return base + rounds * kConvWaves + (wave + i * kConvWaves) / 4; },
       [&](int i) { return (wave + i * kConvWaves) % 4; });
 }
 

@@ -69,17 +69,19 @@ void launch(float* x, const float* b, const float* r, int64_t n, int C, hipStrea
 // ResNet heads (blokus_nnet.py:146-150, BN folded), one 256-thread workgroup per board:
 //   policy features pf[c*NN + i] = relu(x_i . wp_c + bp_c), c = 0, 1 (the NCHW flatten order the
 //   policy Linear expects), and the value MLP v = tanh(W2 relu(W1 relu(x . wv + bv) + b1) + b2).
-// 16 lanes read one pixel's 64-channel row (256 B contiguous) and reduce their partial dot
-// products with DPP row shifts; the value features stay in LDS for the two small layers.
+// Phase 1: 16 lanes read one pixel's 64-channel row (256 B contiguous), several rows in flight
+// per lane, and reduce their partial dot products within the 16-lane row. Phase 2 (fc1): lane o
+// of each wave owns hidden unit o and sweeps a quarter of the NN inputs over the transposed
+// weights w1t [NN][64] (coalesced), the 4 waves' partial sums meet in LDS. Phase 3: one wave.
 constexpr int kHeadC = 64;
 __global__ __launch_bounds__(256) void k_resnet_heads(const float* __restrict__ x, int NN,
                                                       const float* __restrict__ wp, const float* __restrict__ bp,
                                                       const float* __restrict__ wv, const float* __restrict__ bv,
-                                                      const float* __restrict__ w1, const float* __restrict__ b1,
+                                                      const float* __restrict__ w1t, const float* __restrict__ b1,
                                                       const float* __restrict__ w2, const float* __restrict__ b2,
                                                       int P, float* __restrict__ pf, float* __restrict__ vout) {
-  extern __shared__ float vfeat[];  // [NN] value features, then [64] hidden
-  float* hid = vfeat + NN;
+  extern __shared__ float vfeat[];  // [NN] value features, then [4][64] fc1 partial sums
+  float* part = vfeat + NN;
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const int sub = t & 15, grp = t >> 4;  // 16 pixel groups of 16 lanes
@@ -87,43 +89,46 @@ __global__ __launch_bounds__(256) void k_resnet_heads(const float* __restrict__ 
   const float4 wp1 = reinterpret_cast<const float4*>(wp + kHeadC)[sub];
   const float4 wvv = reinterpret_cast<const float4*>(wv)[sub];
   const float* xb = x + (size_t)b * NN * kHeadC;
-  for (int i0 = 0; i0 < NN; i0 += 16) {
-    const int i = i0 + grp;
-    float d0 = 0.f, d1 = 0.f, dv = 0.f;
-    if (i < NN) {
-      const float4 xv = reinterpret_cast<const float4*>(xb + (size_t)i * kHeadC)[sub];
-      d0 = xv.x * wp0.x + xv.y * wp0.y + xv.z * wp0.z + xv.w * wp0.w;
-      d1 = xv.x * wp1.x + xv.y * wp1.y + xv.z * wp1.z + xv.w * wp1.w;
-      dv = xv.x * wvv.x + xv.y * wvv.y + xv.z * wvv.z + xv.w * wvv.w;
-    }
-    // sum over the 16 lanes of the group (xor butterflies stay inside the 16-lane row)
+  constexpr int kIn = 5;  // rows in flight per lane
+  for (int i0 = 0; i0 < NN; i0 += 16 * kIn) {
+    float4 xv[kIn];
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) {
-      d0 += __shfl_xor(d0, o, 16);
-      d1 += __shfl_xor(d1, o, 16);
-      dv += __shfl_xor(dv, o, 16);
+    for (int u = 0; u < kIn; ++u) {
+      const int i = i0 + 16 * u + grp;
+      xv[u] = i < NN ? reinterpret_cast<const float4*>(xb + (size_t)i * kHeadC)[sub] : float4{0.f, 0.f, 0.f, 0.f};
     }
-    if (sub == 0 && i < NN) {
-      pf[(size_t)b * 2 * NN + i] = fmaxf(d0 + bp[0], 0.0f);
-      pf[(size_t)b * 2 * NN + NN + i] = fmaxf(d1 + bp[1], 0.0f);
-      vfeat[i] = fmaxf(dv + bv[0], 0.0f);
+#pragma unroll
+    for (int u = 0; u < kIn; ++u) {
+      const int i = i0 + 16 * u + grp;
+      float d0 = xv[u].x * wp0.x + xv[u].y * wp0.y + xv[u].z * wp0.z + xv[u].w * wp0.w;
+      float d1 = xv[u].x * wp1.x + xv[u].y * wp1.y + xv[u].z * wp1.z + xv[u].w * wp1.w;
+      float dv = xv[u].x * wvv.x + xv[u].y * wvv.y + xv[u].z * wvv.z + xv[u].w * wvv.w;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) {
+        d0 += __shfl_xor(d0, o, 16);
+        d1 += __shfl_xor(d1, o, 16);
+        dv += __shfl_xor(dv, o, 16);
+      }
+      if (sub == 0 && i < NN) {
+        pf[(size_t)b * 2 * NN + i] = fmaxf(d0 + bp[0], 0.0f);
+        pf[(size_t)b * 2 * NN + NN + i] = fmaxf(d1 + bp[1], 0.0f);
+        vfeat[i] = fmaxf(dv + bv[0], 0.0f);
+      }
     }
   }
   __syncthreads();
-  // fc1: 64 outputs, one wave per 16 of them, lanes over the NN inputs
   const int wave = t >> 6, l = t & 63;
-  for (int o = wave * 16; o < wave * 16 + 16; ++o) {
-    float acc = 0.f;
-    for (int i = l; i < NN; i += kWave) acc += w1[(size_t)o * NN + i] * vfeat[i];
-    acc = wave_sum_f(acc);
-    if (l == 0) hid[o] = fmaxf(acc + b1[o], 0.0f);
-  }
+  const int q0 = (NN * wave) / 4, q1 = (NN * (wave + 1)) / 4;
+  float acc = 0.f;
+#pragma unroll 4
+  for (int i = q0; i < q1; ++i) acc += w1t[(size_t)i * kHeadC + l] * vfeat[i];
+  part[wave * kHeadC + l] = acc;
   __syncthreads();
   if (wave == 0) {
+    const float h = fmaxf(((part[l] + part[kHeadC + l]) + (part[2 * kHeadC + l] + part[3 * kHeadC + l])) + b1[l], 0.0f);
     for (int q = 0; q < P; ++q) {
-      float acc = w2[q * kHeadC + l] * hid[l];
-      acc = wave_sum_f(acc);
-      if (l == 0) vout[(size_t)b * P + q] = tanhf(acc + b2[q]);
+      const float s = wave_sum_f(w2[q * kHeadC + l] * h);
+      if (l == 0) vout[(size_t)b * P + q] = tanhf(s + b2[q]);
     }
   }
 }
@@ -150,15 +155,15 @@ int bk_bias_act(float* x, int64_t n, int C, const float* bias, const float* resi
 }
 
 int bk_resnet_heads(const float* x, int B, int NN, const float* wp, const float* bp, const float* wv, const float* bv,
-                    const float* w1, const float* b1, const float* w2, const float* b2, int P, float* pf,
+                    const float* w1t, const float* b1, const float* w2, const float* b2, int P, float* pf,
                     float* vout, void* stream) {
-  BK_REQUIRE(x && wp && bp && wv && bv && w1 && b1 && w2 && b2 && pf && vout && B >= 0 && NN > 0 && P > 0,
+  BK_REQUIRE(x && wp && bp && wv && bv && w1t && b1 && w2 && b2 && pf && vout && B >= 0 && NN > 0 && P > 0,
              "bad argument");
   BK_REQUIRE(((uintptr_t)x & 15u) == 0 && ((uintptr_t)wp & 15u) == 0 && ((uintptr_t)wv & 15u) == 0,
              "bk_resnet_heads: 16-byte aligned x, wp, wv");
   if (B == 0) return BK_OK;
-  hipLaunchKernelGGL(k_resnet_heads, dim3(B), dim3(256), sizeof(float) * (NN + kHeadC), (hipStream_t)stream, x, NN,
-                     wp, bp, wv, bv, w1, b1, w2, b2, P, pf, vout);
+  hipLaunchKernelGGL(k_resnet_heads, dim3(B), dim3(256), sizeof(float) * (NN + 4 * kHeadC), (hipStream_t)stream, x, NN,
+                     wp, bp, wv, bv, w1t, b1, w2, b2, P, pf, vout);
   return launch_check("k_resnet_heads");
 }
 

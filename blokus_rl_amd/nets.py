@@ -140,6 +140,13 @@ class FusedResNet(nn.Module):
         self.value_conv = _fold_bn(net.value_conv, net.value_bn)
         self.value_fc1 = net.value_fc1
         self.value_fc2 = net.value_fc2
+        self._fc1_t = None
+
+    def value_fc1_wt(self) -> torch.Tensor:
+        """value_fc1.weight transposed to [N*N, 64] (bk_resnet_heads' layout), cached."""
+        if self._fc1_t is None:
+            self._fc1_t = self.value_fc1.weight.detach().float().t().contiguous()
+        return self._fc1_t
 
     def forward(self, x):
         x = F.relu(self.stem(x))
@@ -214,7 +221,7 @@ def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
     c = lambda t: t.detach().float().contiguous()  # noqa: E731
     wp, wv = c(f.policy_conv.weight.view(2, 64)), c(f.value_conv.weight.view(64))
     _check(load_library().bk_resnet_heads(ctypes.c_void_p(x.data_ptr()), B, N * N, _ptr(wp), _ptr(c(f.policy_conv.bias)),
-                                          _ptr(wv), _ptr(c(f.value_conv.bias)), _ptr(c(f.value_fc1.weight)),
+                                          _ptr(wv), _ptr(c(f.value_conv.bias)), _ptr(f.value_fc1_wt()),
                                           _ptr(c(f.value_fc1.bias)), _ptr(c(f.value_fc2.weight)),
                                           _ptr(c(f.value_fc2.bias)), P, _ptr(pf), _ptr(v), _stream(x.device)))
     return pf, v

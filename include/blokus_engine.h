@@ -238,9 +238,9 @@ int bk_conv3x3_packed_floats(int cin);
 /* The ResNet heads (blokus_nnet.py:146-150, BN folded) from the tower output x [B][NN][64] NHWC:
  * pf[B][2*NN] = relu(1x1 conv 64->2 + bp) flattened channel-major (the policy Linear's input),
  * v[B][P] = tanh(W2 relu(W1 relu(1x1 conv 64->1 + bv) + b1) + b2); wp [2][64], wv [64],
- * w1 [64][NN], w2 [P][64] (row-major, torch layouts). */
+ * w1t [NN][64] (value_fc1.weight transposed), w2 [P][64] (row-major). */
 int bk_resnet_heads(const float* x, int B, int NN, const float* wp, const float* bp, const float* wv, const float* bv,
-                    const float* w1, const float* b1, const float* w2, const float* b2, int P, float* pf,
+                    const float* w1t, const float* b1, const float* w2, const float* b2, int P, float* pf,
                     float* vout, void* stream);
 int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, const float* bias, const float* residual,
                int relu, float* y, void* stream);

@@ -1,0 +1,29 @@
+"""Fold rocprofv3 --pmc pass directories into a profiles/*pmc*.json entry that bench.py reads
+(_pmc_traffic): per-dispatch means of every counter for kernels whose name contains <pattern>,
+HBM bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (the gfx950 FETCH_SIZE correction of
+MI355X_MICROARCH.md §HBM; both counters are in KB).
+usage: python tools/pmc_to_json.py <out.json> <key> <pattern> <units_per_launch> <algorithmic_bytes> <note> <pass dirs...>"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+out, key, pat, units, algo, note = sys.argv[1:7]
+dirs = sys.argv[7:]
+acc = collections.defaultdict(list)
+for d in dirs:
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if pat in r.get("Kernel_Name", ""):
+                acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+means = {k: sum(v) / len(v) for k, v in acc.items()}
+fetch = 2 * means.get("FETCH_SIZE", 0.0) * 1024
+write = means.get("WRITE_SIZE", 0.0) * 1024
+doc = json.load(open(out)) if os.path.exists(out) else {"round": 1, "kernels": {}}
+doc.setdefault("notes", {})[key] = note
+doc["kernels"][key] = {"units_per_launch": int(units), "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch,
+                       "write_bytes": write, "algorithmic_bytes": int(float(algo)), "counters_per_dispatch": means}
+json.dump(doc, open(out, "w"), indent=1)
+print(key, {k: round(v, 1) for k, v in doc["kernels"][key].items() if k != "counters_per_dispatch"})
