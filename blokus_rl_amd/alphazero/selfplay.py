@@ -127,12 +127,36 @@ class SelfPlay:
         self.active = torch.ones(games, dtype=torch.int32, device=dev)
         self.first_ply = torch.ones(games, dtype=torch.bool, device=dev)
         self.game_id = torch.arange(games, dtype=torch.int64, device=dev)
-        self.next_game_id = games
-        self.stats = SelfPlayStats()
-        self._pending: list[tuple[torch.Tensor, ...]] = []  # per-ply records awaiting z
+        self._stats = SelfPlayStats()
+        # device-side bookkeeping: no host sync anywhere in play_ply
+        self._next_gid = torch.full((), games, dtype=torch.int64, device=dev)
+        self._sims_dev = torch.zeros((), dtype=torch.int64, device=dev)
+        self._fin_dev = torch.zeros((), dtype=torch.int64, device=dev)
+        self._zcap = 0
+        self.z_table = torch.zeros((0, eng.P), dtype=torch.float32, device=dev)  # z of game id g
+        self.z_known = torch.zeros(0, dtype=torch.bool, device=dev)
+        self._ensure_zcap()
+        self._records: list[tuple[torch.Tensor, ...]] = []  # per-ply records (z resolved lazily)
         self.timers = None
-        self.finished: list[Examples] = []
         self._window: list[tuple[torch.Tensor, ...]] = []  # records since mark_window()
+
+    @property
+    def stats(self) -> SelfPlayStats:
+        """Host copy of the counters (synchronises the stream once)."""
+        self._stats.sims = int(self._sims_dev.item())
+        self._stats.games_finished = int(self._fin_dev.item())
+        return self._stats
+
+    def _ensure_zcap(self):
+        """z_table rows for every game id that can exist after the next ply (ids < G*(plies+2))."""
+        need = self.G * (self._stats.plies + 2)
+        if need > self._zcap:
+            cap = max(need, 2 * self._zcap)
+            dev = self.eng.device
+            self.z_table = torch.cat([self.z_table, torch.zeros((cap - self._zcap, self.eng.P), dtype=torch.float32,
+                                                                device=dev)])
+            self.z_known = torch.cat([self.z_known, torch.zeros(cap - self._zcap, dtype=torch.bool, device=dev)])
+            self._zcap = cap
 
     # ------------------------------------------------------------------ one simulation
     def simulate(self):
@@ -174,14 +198,14 @@ class SelfPlay:
         col = torch.arange(cap, device=self.eng.device).unsqueeze(0)
         valid = col < counts.clamp(min=0).unsqueeze(1)
         pi = torch.where(valid, pi, torch.zeros_like(pi))
-        # root-only Dirichlet noise on each game's first ply (trainer.py:110-116)
-        if bool(self.first_ply.any()):
-            gam = torch._standard_gamma(torch.full((G, cap), self.alpha, dtype=torch.float64,
-                                                   device=self.eng.device), generator=self.gen)
-            gam = torch.where(valid, gam, torch.zeros_like(gam))
-            noise = gam / gam.sum(dim=1, keepdim=True).clamp(min=1e-300)
-            mixed = pi * (1 - self.weight) + noise * self.weight
-            pi = torch.where(self.first_ply.unsqueeze(1), mixed, pi)
+        # root-only Dirichlet noise on each game's first ply (trainer.py:110-116); drawn every
+        # ply and applied where first_ply, so no host round trip decides it
+        gam = torch._standard_gamma(torch.full((G, cap), self.alpha, dtype=torch.float64,
+                                               device=self.eng.device), generator=self.gen)
+        gam = torch.where(valid, gam, torch.zeros_like(gam))
+        noise = gam / gam.sum(dim=1, keepdim=True).clamp(min=1e-300)
+        mixed = pi * (1 - self.weight) + noise * self.weight
+        pi = torch.where(self.first_ply.unsqueeze(1), mixed, pi)
         pi32 = pi.to(torch.float32)
         act_mask = self.active.bool() & (counts > 0)
         probs = torch.where(act_mask.unsqueeze(1), pi32, (col == 0).to(torch.float32))
@@ -192,45 +216,34 @@ class SelfPlay:
             player = Engine.to_move(self.roots).clone()
             rec = (self.roots.clone(), ids.to(torch.int16), pi32, counts.clone(), player, self.game_id.clone(),
                    act_mask.clone())
-            self._pending.append(rec)
+            self._records.append(rec)
             self._window.append(rec)
         self.roots, _, status = self.eng.next_state(self.roots, action)
         self.first_ply &= ~act_mask
-        self.stats.plies += 1
-        self.stats.sims += int(self.num_sims) * int(act_mask.sum().item())
+        self._stats.plies += 1
+        self._sims_dev += int(self.num_sims) * act_mask.sum()
         ended, scores = self.eng.game_ended(self.roots)
         done = ended.bool() & self.active.bool()
-        if bool(done.any()):
-            self._finish(done, scores)
+        self._finish(done, scores)
         return status
 
     def _finish(self, done: torch.Tensor, scores: torch.Tensor):
-        """Assign z to every pending example of the finished games; reset/restart their trees."""
-        self.stats.games_finished += int(done.sum().item())
-        fin_ids = self.game_id[done]
-        z_of = {}
-        for gid, sc in zip(fin_ids.tolist(), scores[done].float()):
-            z_of[gid] = sc
-        keep = []
-        for rec in self._pending:
-            states, ids, pi, k, player, gids, m = rec
-            sel = m & torch.isin(gids, fin_ids)
-            if bool(sel.any()):
-                zs = torch.stack([z_of[g] for g in gids[sel].tolist()])
-                self.finished.append(Examples(states[sel], ids[sel], pi[sel], k[sel], zs))
-                m = m & ~sel
-            if bool(m.any()):
-                keep.append((states, ids, pi, k, player, gids, m))
-        self._pending = keep
+        """Record z of the games that ended this ply (z_table[game id]); reset their trees and,
+        in continuous mode, start new games in their slots. Masked device ops only."""
+        self._ensure_zcap()
+        gid = self.game_id
+        self.z_table[gid] = torch.where(done.unsqueeze(1), scores.float(), self.z_table[gid])
+        self.z_known[gid] = self.z_known[gid] | done
+        self._fin_dev += done.sum()
         flags = done.to(torch.int32)
-        self.mcts.reset(flags)  # a new MCTS per episode (trainer.py:95)
+        self.mcts.reset(flags)  # a new MCTS per episode (trainer.py:95); no-op for unflagged trees
         if self.continuous:
             fresh = self.eng.init_states(self.G)
             self.roots = torch.where(done.unsqueeze(1), fresh, self.roots)
             self.first_ply |= done
-            n = int(done.sum().item())
-            self.game_id[done] = torch.arange(self.next_game_id, self.next_game_id + n, device=self.eng.device)
-            self.next_game_id += n
+            d = done.to(torch.int64)
+            self.game_id = torch.where(done, self._next_gid + torch.cumsum(d, 0) - 1, self.game_id)
+            self._next_gid += d.sum()
         else:
             self.active = self.active & ~flags
 
@@ -255,18 +268,36 @@ class SelfPlay:
         z = torch.zeros((states.shape[0], self.eng.P), dtype=torch.float32, device=self.eng.device)
         return pack(states, ids, pi, k, z, player, cap=cap)
 
-    def run(self, plies: int):
+    def run(self, plies: int, check_every: int = 8):
+        """Up to `plies` plies; in finite mode stops once every game is over (checked every
+        `check_every` plies — extra plies of finished games are no-ops)."""
         t0 = time.perf_counter()
-        for _ in range(plies):
-            if not bool(self.active.any()):
+        for i in range(plies):
+            if not self.continuous and i % check_every == 0 and not bool(self.active.any()):
                 break
             self.play_ply()
         torch.cuda.synchronize(self.eng.device)
-        self.stats.seconds += time.perf_counter() - t0
+        self._stats.seconds += time.perf_counter() - t0
         return self.stats
 
-    def examples(self) -> Examples | None:
-        if not self.finished:
+    def examples(self, drain: bool = False) -> Examples | None:
+        """Every recorded example of a finished game (z known), in ply order. drain=True drops
+        them from the record list (records of running games stay)."""
+        if not self._records:
             return None
-        return Examples(*(torch.cat([getattr(e, f) for e in self.finished]) for f in
-                          ("states", "ids", "pi", "k", "z")))
+        m = torch.cat([r[6] for r in self._records])
+        gids = torch.cat([r[5] for r in self._records])
+        sel = m & self.z_known[gids]
+        if not bool(sel.any()):
+            return None
+        ex = Examples(torch.cat([r[0] for r in self._records])[sel], torch.cat([r[1] for r in self._records])[sel],
+                      torch.cat([r[2] for r in self._records])[sel], torch.cat([r[3] for r in self._records])[sel],
+                      self.z_table[gids[sel]])
+        if drain:
+            keep = []
+            for r in self._records:
+                mr = r[6] & ~self.z_known[r[5]]
+                if bool(mr.any()):
+                    keep.append(r[:6] + (mr,))
+            self._records = keep
+        return ex
