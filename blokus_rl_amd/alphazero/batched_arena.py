@@ -80,7 +80,8 @@ class BatchedArena:
         orders = torch.tensor([matches[i % len(matches)] for i in range(G)], dtype=torch.int64, device=dev)  # [G,P]
         T = G * P
         mcts = BatchedMCTS(eng, T, node_cap=self.node_cap, child_cap=T * self.child_cap_per_tree)
-        evals = [LeafEvaluator(m, eng, G, self.nn_dtype, use_graph=m is not None) for m in self._models]
+        evals = [LeafEvaluator(m, eng, G, self.nn_dtype, use_graph=m is not None, sparse_policy=False)
+                 for m in self._models]
         seat_net = torch.tensor(self.seat_net, dtype=torch.int64, device=dev)
         seat_sims = torch.tensor([s.simulations for s in self.seats], dtype=torch.int64, device=dev)
         max_sims = max(s.simulations for s in self.seats)

@@ -55,10 +55,21 @@ class BatchedMCTS:
                                        _ptr(self.obs), _ptr(self.leaf_mask), self._s()))
         return self.status, self.obs, self.leaf_mask
 
-    def expand_backup(self, logp: torch.Tensor, values: torch.Tensor, prior_mode: int = 0):
-        assert logp.dtype == torch.float32 and values.dtype == torch.float32
-        assert logp.shape == (self.T, self.eng.A) and values.shape == (self.T, self.eng.P)
+    def expand_backup(self, logp: torch.Tensor | None, values: torch.Tensor, prior_mode: int = 0):
+        """prior_mode 0: dense logits/log-probs [T, A]; 1: priors at the legal ids (test hook);
+        2: the sparse logits of leaf_logits() (logp None)."""
+        assert values.dtype == torch.float32 and values.shape == (self.T, self.eng.P)
+        if prior_mode != 2:
+            assert logp.dtype == torch.float32 and logp.shape == (self.T, self.eng.A)
         _check(self.lib.bk_mcts_expand_backup(self.h, _ptr(logp), _ptr(values), prior_mode, self._s()))
+
+    def leaf_logits(self, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor):
+        """Policy logits of each leaf's legal ids only (bk_mcts_leaf_logits): feat [T, F] f32,
+        weight [A, F], bias [A] — the policy head's last Linear — for expand_backup(mode 2)."""
+        assert feat.dtype == torch.float32 and feat.shape[0] == self.T and feat.stride(1) == 1
+        assert weight.is_contiguous() and weight.shape == (self.eng.A, feat.shape[1]) and bias.shape == (self.eng.A,)
+        _check(self.lib.bk_mcts_leaf_logits(self.h, ctypes.c_void_p(feat.data_ptr()), feat.stride(0), feat.shape[1],
+                                            _ptr(weight), _ptr(bias), self._s()))
 
     def root_policy(self, roots: torch.Tensor, active: torch.Tensor | None, temperature: float, cap: int = 2048):
         ids = torch.zeros((self.T, cap), dtype=torch.int32, device=self.eng.device)

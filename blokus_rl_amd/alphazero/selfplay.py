@@ -49,10 +49,11 @@ class LeafEvaluator:
     v [G, P] f32). DumbNet needs no forward: a constant uniform log-prior and zero values."""
 
     def __init__(self, model: torch.nn.Module | None, eng: Engine, G: int, dtype: torch.dtype = torch.float32,
-                 use_graph: bool = True):
+                 use_graph: bool = True, sparse_policy: bool = True):
         self.model = model
         self.eng = eng
         self.G = G
+        self.sparse = False
         self.dtype = dtype
         dev = eng.device
         self.const_logp = None
@@ -62,9 +63,19 @@ class LeafEvaluator:
             self.const_v = torch.zeros((G, eng.P), dtype=torch.float32, device=dev)
             self.model = None
             return
-        from ..nets import inference_model
-        # raw policy logits are enough: k_expand_backup takes the softmax over the legal ids
-        self.model = inference_model(model, normalize=False, dtype=dtype).to(memory_format=torch.channels_last)
+        from ..nets import LeafResNet, inference_model
+        # raw policy logits are enough: k_expand_backup takes the softmax over the legal ids; with
+        # the HIP ResNet, even the policy Linear is left to the search (bk_mcts_leaf_logits computes
+        # only the leaf's legal ids' logits), so the net returns (policy features, v)
+        self.model = inference_model(model, normalize=False, dtype=dtype, features=sparse_policy).to(
+            memory_format=torch.channels_last)
+        self.sparse = isinstance(self.model, LeafResNet) and self.model.native and sparse_policy
+        if isinstance(self.model, LeafResNet) and not self.sparse:
+            self.model.features = False
+        if self.sparse:
+            po = self.model.f.policy_out
+            self.policy_w = po.weight.detach().float().contiguous()
+            self.policy_b = po.bias.detach().float().contiguous()
         self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32,
                                       device=dev).contiguous(memory_format=torch.channels_last)
         self.graph = None
@@ -159,13 +170,22 @@ class SelfPlay:
             self._zcap = cap
 
     # ------------------------------------------------------------------ one simulation
+    def _evaluate(self, obs):
+        """Net on the leaf batch, leaving the priors' inputs in the search state: dense logits,
+        or (HIP ResNet) policy features + the sparse policy head over the legal ids."""
+        out, v = self.evaluator(obs)
+        if self.evaluator.sparse:
+            self.mcts.leaf_logits(out, self.evaluator.policy_w, self.evaluator.policy_b)
+            return None, v, 2
+        return out, v, 0
+
     def simulate(self):
         """One simulation in every active tree (= num active trees simulate() calls)."""
         if self.timers is not None:
             return self._simulate_timed()
         _, obs, _ = self.mcts.select(self.roots, self.active, self.cpuct)
-        logp, v = self.evaluator(obs)
-        self.mcts.expand_backup(logp, v, prior_mode=0)
+        logp, v, mode = self._evaluate(obs)
+        self.mcts.expand_backup(logp, v, prior_mode=mode)
 
     def enable_timers(self, on: bool = True):
         """HIP events around each stage on the launch stream (bench.py roofline inputs)."""
@@ -177,9 +197,9 @@ class SelfPlay:
         ev[0].record(st)
         _, obs, _ = self.mcts.select(self.roots, self.active, self.cpuct)
         ev[1].record(st)
-        logp, v = self.evaluator(obs)
+        logp, v, mode = self._evaluate(obs)
         ev[2].record(st)
-        self.mcts.expand_backup(logp, v, prior_mode=0)
+        self.mcts.expand_backup(logp, v, prior_mode=mode)
         ev[3].record(st)
         self.timers["select"].append((ev[0], ev[1]))
         self.timers["net"].append((ev[1], ev[2]))

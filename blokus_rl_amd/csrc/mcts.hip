@@ -27,6 +27,9 @@ namespace bk {
 constexpr int kMaxDepth = 96;
 constexpr int kExpandLdsIds = 2048;  // leaf ids staged in LDS up to this K
 constexpr int kGatherRegs = 16;      // logits gathered into registers: K <= 1024 in one round
+constexpr int kLeafCap = 2048;       // sparse leaf policy: legal ids per leaf (bk_mcts_leaf_logits)
+constexpr int kLeafBlocks = 4;       // workgroups per tree in k_leaf_logits
+constexpr int kMaxFeat = 2048;       // policy-feature length staged in LDS
 
 // Diagnostic build only (-DBK_STAMPS, `make diag`): per-tree s_memtime stamps at phase
 // boundaries of k_select / k_expand_backup; never compiled into the shipped library.
@@ -60,11 +63,14 @@ struct DevMcts {
   int32_t* leaf_status; // [T]
   double* leaf_scores;  // [T*kMaxP]
   uint64_t* leaf_mask;  // [T*W64] internal copy of the leaf bitmask
+  int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
+  float* leaf_logit;    // [T*kLeafCap] their logits
+  int32_t* leaf_K;      // [T]
   unsigned long long* counters;  // [8]
 };
 
 enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5, kCtrScanned = 6, kCtrLeafK = 7 };
-enum { kErrChildPool = 1, kErrTable = 2, kErrDepth = 4, kErrIllegal = 8, kErrMissingRoot = 16 };
+enum { kErrChildPool = 1, kErrTable = 2, kErrDepth = 4, kErrIllegal = 8, kErrMissingRoot = 16, kErrLeafCap = 32 };
 
 __device__ __forceinline__ uint64_t table_key(const uint32_t* s) {
   const uint64_t h = state_hash(s);
@@ -251,8 +257,93 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
   }
 }
 
+// The policy head's last layer restricted to the leaf's legal ids (the only logits the
+// expansion reads): logit[j] = W[id_j] . feat[t] + bias[id_j] for the K legal ids of tree t's
+// leaf, instead of the dense [T, A] Linear (blokus_nnet.py:147-148) — K ~ 200 of A = 30433.
+// kLeafBlocks workgroups per tree each compact the leaf bitmask (ascending ids) and take a
+// contiguous share of the ids; a wave computes one dot product at a time over the feature row
+// staged in LDS, W rows read as coalesced float4s.
+__global__ __launch_bounds__(256) void k_leaf_logits(DevPreset dp, DevMcts m, const float* __restrict__ feat,
+                                                     int64_t ldf, int F, const float* __restrict__ W,
+                                                     const float* __restrict__ bias) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* m32 = lds;                                                   // W32pad words
+  int32_t* ids = reinterpret_cast<int32_t*>(lds + dp.W32pad);            // kLeafCap
+  float* f = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap);       // F (16-B aligned: W32pad % 4 == 0)
+  __shared__ int Ksh;
+  const int t = blockIdx.x, c = blockIdx.y;
+  if (m.leaf_status[t] != 1) return;  // block-uniform: no leaf to evaluate
+  const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
+  for (int j = threadIdx.x; j < dp.W64; j += blockDim.x) {
+    const uint64_t w = lm[j];
+    m32[2 * j] = (uint32_t)w;
+    m32[2 * j + 1] = (uint32_t)(w >> 32);
+  }
+  const float* ft = feat + (size_t)t * ldf;
+  for (int i = threadIdx.x; i < F; i += blockDim.x) f[i] = ft[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (wave == 0) {
+    const int K = compact_ids(dp, m32, ids, kLeafCap);
+    if (l == 0) Ksh = K;
+  }
+  __syncthreads();
+  const int K = Ksh;
+  if (c == 0 && threadIdx.x == 0) {
+    m.leaf_K[t] = K;
+    if (K > kLeafCap) atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrLeafCap);
+  }
+  if (K > kLeafCap) return;
+  const int lo = (int)((int64_t)K * c / kLeafBlocks), hi = (int)((int64_t)K * (c + 1) / kLeafBlocks);
+  int32_t* out_ids = m.leaf_ids + (size_t)t * kLeafCap;
+  float* out_lg = m.leaf_logit + (size_t)t * kLeafCap;
+  const int nw = blockDim.x >> 6;
+  if ((F & 3) == 0) {
+    const int F4 = F >> 2;
+    const float4* f4 = reinterpret_cast<const float4*>(f);
+    for (int j = lo + wave; j < hi; j += 2 * nw) {
+      // two ids per pass: both rows' loads in flight together
+      const int j2 = j + nw;
+      const int id = ids[j];
+      const int id2 = j2 < hi ? ids[j2] : id;
+      const float4* r1 = reinterpret_cast<const float4*>(W + (size_t)id * F);
+      const float4* r2 = reinterpret_cast<const float4*>(W + (size_t)id2 * F);
+      float a1 = 0.f, a2 = 0.f;
+      for (int q = l; q < F4; q += kWave) {
+        const float4 w1 = r1[q], w2 = r2[q], x = f4[q];
+        a1 += w1.x * x.x + w1.y * x.y + w1.z * x.z + w1.w * x.w;
+        a2 += w2.x * x.x + w2.y * x.y + w2.z * x.z + w2.w * x.w;
+      }
+      a1 = wave_sum_f(a1);
+      a2 = wave_sum_f(a2);
+      if (l == 0) {
+        out_ids[j] = id;
+        out_lg[j] = a1 + bias[id];
+        if (j2 < hi) {
+          out_ids[j2] = id2;
+          out_lg[j2] = a2 + bias[id2];
+        }
+      }
+    }
+  } else {
+    for (int j = lo + wave; j < hi; j += nw) {
+      const int id = ids[j];
+      const float* r = W + (size_t)id * F;
+      float a = 0.f;
+      for (int q = l; q < F; q += kWave) a += r[q] * f[q];
+      a = wave_sum_f(a);
+      if (l == 0) {
+        out_ids[j] = id;
+        out_lg[j] = a + bias[id];
+      }
+    }
+  }
+}
+
 // prior_mode 0: logp = the net's log-probabilities over all A ids -> masked log-softmax + exp
 //               (get_valid_dist, neural_network.py:159-173);
+// prior_mode 2: the sparse leaf logits of k_leaf_logits (ids + logits of the legal ids) ->
+//               the same softmax, no compaction or gather here;
 // prior_mode 1: logp holds the prior itself at the legal ids (test hook: identical P fed to the
 //               reference and to this engine).
 __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, const float* __restrict__ logp,
@@ -266,27 +357,37 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
   if (status == 0) return;
   BK_STAMP(1, 0);
   if (status == 1) {
-    const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
-    for (int j = l; j < dp.W64; j += kWave) {
-      const uint64_t w = lm[j];
-      m32[2 * j] = (uint32_t)w;
-      m32[2 * j + 1] = (uint32_t)(w >> 32);
-    }
-    __syncthreads();
+    const bool sparse = prior_mode == 2;
     int err = 0;
     const int node = m.tree_nodes[t];
     const int64_t used = m.tree_children[t];
     const int64_t room = m.child_cap_per_tree - used;
     const int64_t off = (int64_t)t * m.child_cap_per_tree + used;
-    // legal ids, ascending (np.where order, mcts.py:64): into LDS when K fits, else straight
-    // into the tree's child region
     int32_t* ids_lds = reinterpret_cast<int32_t*>(m32 + dp.W32pad);
     const int cap_lds = kExpandLdsIds;
+    int K;
+    bool in_lds;
     BK_STAMP(1, 1);
-    int K = compact_ids(dp, m32, ids_lds, cap_lds);
-    const bool in_lds = K <= cap_lds;
-    if (!in_lds) K = compact_ids(dp, m32, m.ch_id + off, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
-    __syncthreads();
+    if (sparse) {
+      K = m.leaf_K[t];
+      in_lds = true;  // the ids are in leaf_ids: write them into the child region below
+      if (K > kLeafCap) err |= kErrLeafCap;
+    } else {
+      const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
+      for (int j = l; j < dp.W64; j += kWave) {
+        const uint64_t w = lm[j];
+        m32[2 * j] = (uint32_t)w;
+        m32[2 * j + 1] = (uint32_t)(w >> 32);
+      }
+      __syncthreads();
+      // legal ids, ascending (np.where order, mcts.py:64): into LDS when K fits, else straight
+      // into the tree's child region
+      K = compact_ids(dp, m32, ids_lds, cap_lds);
+      in_lds = K <= cap_lds;
+      if (!in_lds)
+        K = compact_ids(dp, m32, m.ch_id + off, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
+      __syncthreads();
+    }
     BK_STAMP(1, 2);
     if (node >= m.node_cap) err |= kErrTable;
     if (K > room) err |= kErrChildPool;
@@ -298,26 +399,28 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
     }
     BK_STAMP(1, 3);
     if (!err) {
-      const float* lp = logp + (size_t)t * dp.A;
-      const int32_t* cid = in_lds ? ids_lds : m.ch_id + off;
+      // dense modes gather logp[cid[i]]; the sparse mode reads its logits in id order
+      const float* lp = sparse ? m.leaf_logit + (size_t)t * kLeafCap : logp + (size_t)t * dp.A;
+      const int32_t* cid = sparse ? m.leaf_ids + (size_t)t * kLeafCap : (in_lds ? ids_lds : m.ch_id + off);
+      auto logit = [&](int i) { return sparse ? lp[i] : lp[cid[i]]; };
       // all of a lane's gathers issued before any is used (K <= 64 * kGatherRegs)
       float x[kGatherRegs];
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < kGatherRegs; ++j) {
         const int i = l + j * kWave;
-        x[j] = i < K ? lp[cid[i]] : -INFINITY;
+        x[j] = i < K ? logit(i) : -INFINITY;
       }
 #pragma unroll
       for (int j = 0; j < kGatherRegs; ++j) mx = fmaxf(mx, x[j]);
-      for (int i = l + kGatherRegs * kWave; i < K; i += kWave) mx = fmaxf(mx, lp[cid[i]]);
+      for (int i = l + kGatherRegs * kWave; i < K; i += kWave) mx = fmaxf(mx, logit(i));
       float lse = 0.0f;
-      if (prior_mode == 0) {
+      if (prior_mode != 1) {
         mx = wave_max_f(mx);
         float sum = 0.0f;
 #pragma unroll
         for (int j = 0; j < kGatherRegs; ++j) sum += l + j * kWave < K ? expf(x[j] - mx) : 0.0f;
-        for (int i = l + kGatherRegs * kWave; i < K; i += kWave) sum += expf(lp[cid[i]] - mx);
+        for (int i = l + kGatherRegs * kWave; i < K; i += kWave) sum += expf(logit(i) - mx);
         sum = wave_sum_f(sum);
         lse = logf(sum);
 #pragma unroll
@@ -335,11 +438,11 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
         }
       }
       for (int i = l + kGatherRegs * kWave; i < K; i += kWave) {
-        const float xi = lp[cid[i]];
+        const float xi = logit(i);
         if (in_lds) m.ch_id[off + i] = cid[i];
         m.ch_N[off + i] = 0u;
         m.ch_Q[off + i] = 0.0;
-        m.ch_P[off + i] = prior_mode == 0 ? expf((xi - mx) - lse) : xi;
+        m.ch_P[off + i] = prior_mode != 1 ? expf((xi - mx) - lse) : xi;
       }
       if (l == 0) {
         const size_t gn = (size_t)t * m.node_cap + node;
@@ -508,6 +611,9 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
   if (!rc) rc = mcts_alloc(m, &d.leaf_status, T);
   if (!rc) rc = mcts_alloc(m, &d.leaf_scores, T * kMaxP);
   if (!rc) rc = mcts_alloc(m, &d.leaf_mask, T * W64);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_ids, T * kLeafCap);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_logit, T * kLeafCap);
+  if (!rc) rc = mcts_alloc(m, &d.leaf_K, T);
   if (!rc) rc = mcts_alloc(m, &d.counters, 8);
   if (!rc) rc = hip_check(hipMemset(d.counters, 0, 8 * sizeof(unsigned long long)), "memset counters");
   if (!rc) rc = hip_check(hipMemset(d.leaf_status, 0, T * sizeof(int32_t)), "memset status");
@@ -544,8 +650,20 @@ int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double 
   return launch_check("k_select");
 }
 
+int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
+                        void* stream) {
+  BK_REQUIRE(m && feat && W && bias && F > 0 && F <= kMaxFeat && ldf >= F, "bad argument");
+  BK_REQUIRE(((uintptr_t)W & 15u) == 0 || (F & 3) != 0, "bk_mcts_leaf_logits: W must be 16-byte aligned");
+  const DevPreset& dp = m->ctx->dp;
+  const size_t lds = sizeof(uint32_t) * ((size_t)dp.W32pad + kLeafCap + F);
+  hipLaunchKernelGGL(k_leaf_logits, dim3(m->d.T, kLeafBlocks), dim3(256), lds, (hipStream_t)stream, dp, m->d, feat,
+                     ldf, F, W, bias);
+  return launch_check("k_leaf_logits");
+}
+
 int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, int prior_mode, void* stream) {
-  BK_REQUIRE(m && logp && values && (prior_mode == 0 || prior_mode == 1), "bad argument");
+  BK_REQUIRE(m && values && (prior_mode == 0 || prior_mode == 1 || prior_mode == 2), "bad argument");
+  BK_REQUIRE(logp || prior_mode == 2, "bad argument: logp");
   const DevPreset& dp = m->ctx->dp;
   const size_t lds = sizeof(uint32_t) * ((size_t)dp.W32pad + kExpandLdsIds);
   hipLaunchKernelGGL(k_expand_backup, dim3(m->d.T), dim3(kWave), lds, (hipStream_t)stream, dp, m->d, logp, values,

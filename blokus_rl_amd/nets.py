@@ -235,10 +235,11 @@ class LeafResNet(nn.Module):
     comes back as raw logits (the leaf batch's consumer, k_expand_backup, takes a softmax over the
     legal ids, which a per-row shift does not change), skipping the full-row log-softmax."""
 
-    def __init__(self, net: ResNet, normalize: bool = True):
+    def __init__(self, net: ResNet, normalize: bool = True, features: bool = False):
         super().__init__()
         self.f = FusedResNet(net).eval()
         self.normalize = normalize
+        self.features = features  # return (policy features [B, 2*N*N], v): the search applies policy_out
         f = self.f
         self.native = f.stem.out_channels == 64 and f.stem.in_channels in (4, 8, 64)
         if self.native:
@@ -268,6 +269,8 @@ class LeafResNet(nn.Module):
         x = h if n else F.relu(x + x)
         if self.native:
             pf, v = resnet_heads(x, f)
+            if self.features:
+                return pf, v
             logits = f.policy_out(pf)
         else:
             conv1 = lambda t, c: F.conv2d(t, c.weight, None).contiguous(memory_format=torch.channels_last)  # noqa: E731
@@ -278,13 +281,14 @@ class LeafResNet(nn.Module):
         return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
 
 
-def inference_model(model: nn.Module, normalize: bool = True, dtype: torch.dtype = torch.float32) -> nn.Module:
+def inference_model(model: nn.Module, normalize: bool = True, dtype: torch.dtype = torch.float32,
+                    features: bool = False) -> nn.Module:
     """The leaf evaluator's form of a net: ResNet -> LeafResNet (fp32 HIP kernels) on a HIP
     device, FusedResNet for reduced-precision autocast runs or off the device; eval() otherwise.
     normalize=False lets LeafResNet return raw policy logits (see LeafResNet)."""
     if isinstance(model, ResNet):
         dev = next(model.parameters()).device
         if dev.type == "cuda" and dtype == torch.float32:
-            return LeafResNet(model, normalize=normalize).eval()
+            return LeafResNet(model, normalize=normalize, features=features).eval()
         return FusedResNet(model).eval()
     return model.eval()

@@ -144,11 +144,23 @@ int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double 
 /* Expansion + backup (mcts.py:50-56 and :63-70): for status-1 leaves create the node with
  * P = exp(log_softmax(logp[t][legal ids])) (neural_network.py:159-173) and back up
  * values[t][P]; for status-2 leaves back up the terminal scores. logp: [T][A] f32 (the net's
- * log-softmax output, rows of inactive/terminal trees ignored); values: [T][P] f32. */
+ * log-softmax output or raw logits — the softmax over the legal ids is shift-invariant; rows of
+ * inactive/terminal trees ignored); values: [T][P] f32.
+ * prior_mode 0: dense logp as above; 1 (test hook): logp[t][id] already holds the prior P at
+ * the legal ids, no softmax — lets a test feed the reference MCTS and this engine identical
+ * priors; 2: the sparse logits of bk_mcts_leaf_logits (logp may be NULL). */
 int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, int prior_mode,
                           void* stream);
-/* prior_mode 1 (test hook): logp[t][id] already holds the prior P at the legal ids; no softmax.
- * Lets a test feed the reference MCTS and this engine identical priors. */
+
+/* The policy head's last Linear restricted to each leaf's legal ids (prior_mode 2 input):
+ * for every tree whose last select pass stopped at a leaf needing evaluation, logit_j =
+ * W[id_j] . feat[t] + bias[id_j] over the leaf's K legal ids (ascending), kept inside the
+ * search state (K <= 2048, else error bit 32). feat [T][ldf] f32 (the policy features, F of
+ * them), W [A][F], bias [A] (policy_out of models/blokus_nnet.py:147, the same parameters the
+ * dense head multiplies). Replaces the [T, A] GEMM + gather: only the K ~ 200 logits of the
+ * legal ids are computed. */
+int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
+                        void* stream);
 
 /* get_distribution (mcts.py:73-99) at the root of every active tree: ids[t][0..K) and
  * pi[t][0..K) (f64) in child order, K in counts[t]; temperature 0 -> one-hot argmax N

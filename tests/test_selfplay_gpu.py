@@ -54,3 +54,40 @@ def test_selfplay_20x20_resnet_smoke():
     # the roots advanced three plies: 3 pieces placed in every game
     sq = eng.square_counts(sp.roots).cpu().numpy()
     assert (sq.sum(axis=1) > 0).all()
+
+
+def test_sparse_policy_head_matches_dense_priors():
+    """bk_mcts_leaf_logits + expand mode 2 (policy Linear over the legal ids only) gives the
+    priors of the dense head (the [T, A] Linear + masked softmax), to f32 rounding."""
+    import torch
+
+    from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
+    from blokus_rl_amd.boards import random_boards
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import LeafResNet, ResNet
+
+    eng = Engine(20, 4, 5)
+    torch.manual_seed(0)
+    net = ResNet(20, 4, eng.A, 2).cuda().eval()
+    dense = LeafResNet(net, normalize=False).eval()
+    feats = LeafResNet(net, normalize=False, features=True).eval()
+    T = 32
+    roots = random_boards(eng, T, seed0=5, max_plies=30)
+    m1 = BatchedMCTS(eng, T, node_cap=64, child_cap=T * 64 * 700)
+    m2 = BatchedMCTS(eng, T, node_cap=64, child_cap=T * 64 * 700)
+    for _ in range(3):
+        _, obs, _ = m1.select(roots, None, 1.0)
+        _, obs2, _ = m2.select(roots, None, 1.0)
+        assert torch.equal(obs, obs2)
+        lg, v = dense(obs)
+        pf, v2 = feats(obs)
+        m1.expand_backup(lg.contiguous(), v.contiguous(), 0)
+        po = net.policy_out
+        m2.leaf_logits(pf.contiguous(), po.weight.detach().contiguous(), po.bias.detach().contiguous())
+        m2.expand_backup(None, v2.contiguous(), 2)
+    c1, c2 = m1.check(), m2.check()
+    assert c1["expanded"] == c2["expanded"] == 3 * T
+    i1, n1, q1, p1, k1 = m1.root_stats(roots)
+    i2, n2, q2, p2, k2 = m2.root_stats(roots)
+    assert torch.equal(k1, k2) and torch.equal(i1, i2)
+    assert (p1 - p2).abs().max().item() < 1e-6
