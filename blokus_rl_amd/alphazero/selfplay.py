@@ -54,6 +54,7 @@ class LeafEvaluator:
         self.eng = eng
         self.G = G
         self.sparse = False
+        self.planar = False
         self.dtype = dtype
         dev = eng.device
         self.const_logp = None
@@ -76,14 +77,18 @@ class LeafEvaluator:
             po = self.model.f.policy_out
             self.policy_w = po.weight.detach().float().contiguous()
             self.policy_b = po.bias.detach().float().contiguous()
-        self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32,
-                                      device=dev).contiguous(memory_format=torch.channels_last)
+        # the HIP ResNet reads the planar observation k_select writes (the search can write straight
+        # into static_obs: no copy); the MIOpen paths want channels_last
+        self.planar = isinstance(self.model, LeafResNet) and self.model.native
+        self.static_obs = torch.zeros((G,) + eng.obs_shape, dtype=torch.float32, device=dev)
+        if not self.planar:
+            self.static_obs = self.static_obs.contiguous(memory_format=torch.channels_last)
         self.graph = None
         if use_graph:
             self._capture()
 
     def _forward(self, obs):
-        obs = obs.contiguous(memory_format=torch.channels_last)
+        obs = obs.contiguous() if self.planar else obs.contiguous(memory_format=torch.channels_last)
         with torch.inference_mode():
             if self.dtype != torch.float32:
                 with torch.autocast("cuda", dtype=self.dtype):
@@ -108,7 +113,8 @@ class LeafEvaluator:
         if self.model is None:
             return self.const_logp, self.const_v
         if self.graph is not None:
-            self.static_obs.copy_(obs)
+            if obs.data_ptr() != self.static_obs.data_ptr():
+                self.static_obs.copy_(obs)
             self.graph.replay()
             return self.static_lp, self.static_v
         return self._forward(obs)
@@ -131,6 +137,8 @@ class SelfPlay:
         self.continuous = continuous
         self.mcts = BatchedMCTS(eng, games, node_cap=node_cap, child_cap=child_cap)
         self.evaluator = LeafEvaluator(model, eng, games, nn_dtype, use_graph)
+        if getattr(self.evaluator, "planar", False) and self.evaluator.graph is not None:
+            self.mcts.obs = self.evaluator.static_obs  # k_select writes the net's input buffer directly
         dev = eng.device
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)

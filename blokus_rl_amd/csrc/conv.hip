@@ -1,8 +1,8 @@
 // conv.hip — the leaf evaluator's 3x3 convolutions (ResNet of models/blokus_nnet.py:88-151, BN
 // folded) as one fused fp32 MFMA kernel per layer: y = act(conv3x3(x, W) + b (+ r)).
 //
-// Shape: x [B][N][N][CIN] (NHWC, the leaf batch's channels_last layout), W 64 x CIN x 3 x 3,
-// y [B][N][N][64]. As a GEMM: M = B*N*N output pixels, N = 64 channels, K = 9*CIN. At the
+// Shape: x [B][N][N][64] (CIN = 64, NHWC) or [B][CIN][N][N] (CIN = 4, 8: the observation
+// planes), W 64 x CIN x 3 x 3, y [B][N][N][64] (NHWC). As a GEMM: M = B*N*N output pixels, N = 64 channels, K = 9*CIN. At the
 // self-play batch (256 boards of 20x20, CIN = 64) that is 7.55 GFLOP per layer: MFMA-bound.
 //
 // Design (gfx950, f32-in MFMA v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD, exact f32):
@@ -13,8 +13,10 @@
 //  * A wave owns a tile of 16 consecutive output pixels x all 64 channels: 4 independent 16x16
 //    accumulators (dependent-latency 40 cycles < 4 x 32-cycle issue, so the MFMA pipe never
 //    waits on itself). Its A operand comes straight from global memory: per tap, one CIN-wide
-//    row per pixel, read VEC floats at a time (dwordx4 at CIN >= 16) in a K order permuted so
-//    each vector load feeds VEC consecutive k-steps; out-of-board taps read zeros (padding 1).
+//    row per pixel, read as dwordx4 (CIN = 64; planar observation: VEC scalars) in a K order
+//    permuted so each vector load feeds VEC consecutive k-steps; out-of-board taps read zeros
+//    (padding 1). (A channel-blocked [B][4][NN][16] layout, whose loads are 1 KB contiguous,
+//    measured 3-5% slower.)
 //  * XCD-aware tiling: the 8 XCDs each take a contiguous eighth of the pixel tiles (whole boards,
 //    3.2 MB of input at B=256) so a board's rows are fetched into one XCD's L2 and reused there
 //    by all 9 taps; within an XCD each CU takes a contiguous run of tiles (its waves share board
@@ -33,7 +35,13 @@ namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 constexpr int kCout = 64;
-constexpr int kConvThreads = 768;
+#ifndef BK_CONV_THREADS
+#define BK_CONV_THREADS 768
+#endif
+#ifndef BK_CONV_DB
+#define BK_CONV_DB 8
+#endif
+constexpr int kConvThreads = BK_CONV_THREADS;
 constexpr int kConvWaves = kConvThreads / kWave;
 
 template <int VEC>
@@ -58,7 +66,9 @@ struct VecT<4> {
 // 16-channel blocks from block jblk(i), the whole K = 9*CIN reduction. k-steps per tap:
 // S = CIN / 4 (4 k values per 16x16x4 MFMA); lane group g = lane>>4 holds k index g of each
 // step; step s = q*VEC + r reads input channel cin = 4*VEC*q + VEC*g + r (the host packs W in
-// the same order).
+// the same order). Layouts: CIN = 64 input, the output and the residual are NHWC
+// [B][N][N][64] (the leaf batch's channels_last activations); CIN = 4 / 8 input is planar
+// [B][CIN][N][N] (the observation the search writes, read with no layout conversion).
 //
 // Software pipeline over the run's k-steps, carried across tiles (the body is fully unrolled,
 // so every ring slot is a fixed register set and the s_waitcnt counts are exact):
@@ -77,7 +87,7 @@ __device__ __forceinline__ void conv_run(const float* __restrict__ x, const f32x
   constexpr int S = CIN / 4;
   constexpr int Q = CIN / (4 * VEC);
   constexpr int KS = 9 * S;
-  constexpr int DB = S < 8 ? S : 8;  // B prefetch distance in k-steps (divides KS)
+  constexpr int DB = S < BK_CONV_DB ? S : BK_CONV_DB;  // B prefetch distance in k-steps (divides KS)
   static_assert(KS % DB == 0, "ring must wrap at tile boundaries");
   using V = typename VecT<VEC>::T;
   using WT = typename std::conditional<NJ == 4, f32x4, float>::type;
@@ -105,11 +115,21 @@ __device__ __forceinline__ void conv_run(const float* __restrict__ x, const f32x
     const int yy = pp.py + tap / 3 - 1, xx = pp.px + tap % 3 - 1;
     const bool ok = pp.in && yy >= 0 && yy < N && xx >= 0 && xx < N;
     const int yc = ok ? yy : pp.py, xc = ok ? xx : pp.px;
-    const float* src = x + ((int64_t)(pp.b * N + yc) * N + xc) * CIN + VEC * g;
+    const int pix = yc * N + xc;
     kp = ok ? 1.0f : 0.0f;
+    if constexpr (CIN % 16 == 0) {
+      // NHWC input [B][NN][CIN]: channels 16q + 4g .. +3 of the pixel, one float4 per q
+      const float* src = x + ((int64_t)pp.b * npix + pix) * CIN + 4 * g;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      dst[q] = *reinterpret_cast<const V*>(src + 4 * VEC * q);
+      for (int q = 0; q < Q; ++q) dst[q] = *reinterpret_cast<const V*>(src + 16 * q);
+    } else {
+      // planar input [B][CIN][NN] (the observation planes): channels VEC*g .. +VEC-1
+      const float* src = x + ((int64_t)pp.b * CIN + VEC * g) * npix + pix;
+      V v;
+      float* vf = reinterpret_cast<float*>(&v);
+#pragma unroll
+      for (int r = 0; r < VEC; ++r) vf[r] = src[(int64_t)r * npix];
+      dst[0] = v;
     }
   };
   int j0 = jblk(0);

@@ -69,8 +69,8 @@ void launch(float* x, const float* b, const float* r, int64_t n, int C, hipStrea
 // ResNet heads (blokus_nnet.py:146-150, BN folded), one 256-thread workgroup per board:
 //   policy features pf[c*NN + i] = relu(x_i . wp_c + bp_c), c = 0, 1 (the NCHW flatten order the
 //   policy Linear expects), and the value MLP v = tanh(W2 relu(W1 relu(x . wv + bv) + b1) + b2).
-// Phase 1: 16 lanes read one pixel's 64-channel row (256 B contiguous), several rows in flight
-// per lane, and reduce their partial dot products within the 16-lane row. Phase 2 (fc1): lane o
+// Phase 1: 16 lanes read one pixel's 64-channel row (256 B contiguous, NHWC tower output),
+// several rows in flight per lane, and reduce their partial dot products within the 16-lane row. Phase 2 (fc1): lane o
 // of each wave owns hidden unit o and sweeps a quarter of the NN inputs over the transposed
 // weights w1t [NN][64] (coalesced), the 4 waves' partial sums meet in LDS. Phase 3: one wave.
 constexpr int kHeadC = 64;

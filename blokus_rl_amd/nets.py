@@ -194,11 +194,16 @@ def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
 
 def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bool,
             residual: torch.Tensor | None = None) -> torch.Tensor:
-    """bk_conv3x3 on a channels_last activation [B, cin, N, N] -> [B, 64, N, N] channels_last."""
+    """bk_conv3x3: x = planar observation [B, cin, N, N] contiguous (cin 4 / 8) or a 64-channel
+    activation in channels_last memory format (NHWC) -> [B, 64, N, N] channels_last."""
     from .engine import _check, _ptr, _stream, load_library
 
     B, cin, N, _ = x.shape
-    assert x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+    assert x.dtype == torch.float32
+    if cin == 64:
+        assert x.is_contiguous(memory_format=torch.channels_last)
+    else:
+        assert x.is_contiguous()
     y = torch.empty((B, 64, N, N), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
     if residual is not None:
         assert residual.is_contiguous(memory_format=torch.channels_last) and residual.shape == y.shape
@@ -228,10 +233,11 @@ def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
 
 
 class LeafResNet(nn.Module):
-    """The leaf evaluator's ResNet on the device (fp32, channels_last): FusedResNet's function
-    with every 3x3 conv + bias + ReLU (+ the tower's residual) as one bk_conv3x3 launch (fp32
-    MFMA, weights resident in LDS), both heads' 1x1 convs and the whole value MLP in one
-    bk_resnet_heads launch, and the policy Linear in hipBLASLt. With normalize=False the policy
+    """The leaf evaluator's ResNet on the device (fp32): FusedResNet's function with every 3x3
+    conv + bias + ReLU (+ the tower's residual) as one bk_conv3x3 launch (fp32 MFMA, weights
+    resident in LDS, NHWC activations), both heads' 1x1 convs and the whole value MLP
+    in one bk_resnet_heads launch, and the policy Linear in hipBLASLt (or, features=True, left to
+    the search's sparse head). Input: the planar observation [B, 2P, N, N]. With normalize=False the policy
     comes back as raw logits (the leaf batch's consumer, k_expand_backup, takes a softmax over the
     legal ids, which a per-row shift does not change), skipping the full-row log-softmax."""
 
@@ -241,7 +247,7 @@ class LeafResNet(nn.Module):
         self.normalize = normalize
         self.features = features  # return (policy features [B, 2*N*N], v): the search applies policy_out
         f = self.f
-        self.native = f.stem.out_channels == 64 and f.stem.in_channels in (4, 8, 64)
+        self.native = f.stem.out_channels == 64 and f.stem.in_channels in (4, 8)
         if self.native:
             self.register_buffer("w_stem", pack_conv3x3(f.stem.weight.detach()))
             for i, (c1, c2) in enumerate(f.blocks):
@@ -251,33 +257,37 @@ class LeafResNet(nn.Module):
     @torch.no_grad()
     def forward(self, x):
         f = self.f
-        x = x.float().contiguous(memory_format=torch.channels_last)
         n = len(f.blocks)
         if self.native:
-            x = conv3x3(x, self.w_stem, f.stem.bias, True)
+            # planar observation in (as the search writes it), NHWC activations through the tower
+            x = conv3x3(x.float().contiguous(), self.w_stem, f.stem.bias, True)
             h = x
             for i, (c1, c2) in enumerate(f.blocks):
                 h = conv3x3(h, getattr(self, f"w_{i}_1"), c1.bias, True)
                 h = conv3x3(h, getattr(self, f"w_{i}_2"), c2.bias, i + 1 == n, x if i + 1 == n else None)
-        else:
-            conv = lambda t, c: F.conv2d(t, c.weight, None, c.stride, c.padding)  # noqa: E731
-            x = _bias_act(conv(x, f.stem), f.stem.bias, True)
-            h = x
-            for i, (c1, c2) in enumerate(f.blocks):
-                h = _bias_act(conv(h, c1), c1.bias, True)
-                h = _bias_act(conv(h, c2), c2.bias, i + 1 == n, x if i + 1 == n else None)
-        x = h if n else F.relu(x + x)
-        if self.native:
-            pf, v = resnet_heads(x, f)
+            if not n:
+                h = torch.relu(x + x)
+            pf, v = resnet_heads(h, f)
             if self.features:
                 return pf, v
             logits = f.policy_out(pf)
-        else:
-            conv1 = lambda t, c: F.conv2d(t, c.weight, None).contiguous(memory_format=torch.channels_last)  # noqa: E731
-            p = _bias_act(conv1(x, f.policy_conv), f.policy_conv.bias, True)
-            logits = f.policy_out(p.contiguous().flatten(1))
-            v = _bias_act(conv1(x, f.value_conv), f.value_conv.bias, True)
-            v = torch.tanh(f.value_fc2(F.relu(f.value_fc1(v.contiguous().flatten(1)))))
+            return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
+        # other widths: MIOpen convolutions (channels_last) with the bk_bias_act epilogue
+        x = x.float().contiguous(memory_format=torch.channels_last)
+        conv = lambda t, c: F.conv2d(t, c.weight, None, c.stride, c.padding)  # noqa: E731
+        x = _bias_act(conv(x, f.stem), f.stem.bias, True)
+        h = x
+        for i, (c1, c2) in enumerate(f.blocks):
+            h = _bias_act(conv(h, c1), c1.bias, True)
+            h = _bias_act(conv(h, c2), c2.bias, i + 1 == n, x if i + 1 == n else None)
+        x = h if n else F.relu(x + x)
+        conv1 = lambda t, c: F.conv2d(t, c.weight, None).contiguous(memory_format=torch.channels_last)  # noqa: E731
+        p = _bias_act(conv1(x, f.policy_conv), f.policy_conv.bias, True)
+        logits = f.policy_out(p.contiguous().flatten(1))
+        v = _bias_act(conv1(x, f.value_conv), f.value_conv.bias, True)
+        v = torch.tanh(f.value_fc2(F.relu(f.value_fc1(v.contiguous().flatten(1)))))
+        if self.features:
+            return p.contiguous().flatten(1), v
         return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
 
 

@@ -242,8 +242,8 @@ int bk_filter_legal(const float* x, int E, int A, const uint64_t* mask, int mask
 int bk_bias_act(float* x, int64_t n, int C, const float* bias, const float* residual, int relu, void* stream);
 
 /* 3x3 convolution, stride 1, zero padding 1, 64 output channels, with the fused epilogue
- * y = act(conv(x) + bias (+ residual)): x [B][N][N][cin] and y, residual [B][N][N][64] NHWC f32,
- * cin in {4, 8, 64}. wpacked: the 9*cin*64 weights in the kernel's MFMA operand order
+ * y = act(conv(x) + bias (+ residual)), f32. Layouts: cin 64 input, y and residual are NHWC
+ * [B][N][N][64]; cin 4 or 8 input is planar [B][cin][N][N] (the observation). wpacked: the 9*cin*64 weights in the kernel's MFMA operand order
  * (blokus_rl_amd/nets.py pack_conv3x3 documents it); bk_conv3x3_packed_floats(cin) = its length.
  * Replaces conv + BN (folded) + ReLU (+ residual add) of blokus_nnet.py:135-146. */
 int bk_conv3x3_packed_floats(int cin);

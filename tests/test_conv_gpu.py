@@ -1,5 +1,5 @@
-"""bk_conv3x3 (fp32 MFMA 3x3 conv with fused bias / residual / ReLU) against torch's fp32
-convolution (the "plain PyTorch fp32 reference of the same op"), and LeafResNet against the
+"""bk_conv3x3 (fp32 MFMA 3x3 conv with fused bias / residual / ReLU; NHWC activations, planar
+observation input) against torch's fp32 convolution (the "plain PyTorch fp32 reference of the same op"), and LeafResNet against the
 reference-layout ResNet. Tolerance: the MFMA kernel sums K = 9*cin products in a different order
 than MIOpen, so agreement is to f32 rounding: |diff| <= 1e-5 * (sum_k |x_k w_k| + 1) per output."""
 import pytest
@@ -26,17 +26,19 @@ def test_conv3x3_matches_torch(B, N, cin, relu, use_res):
     from blokus_rl_amd.nets import conv3x3, pack_conv3x3
 
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + N * 10 + cin)
-    x = torch.randn((B, cin, N, N), device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+    x = torch.randn((B, cin, N, N), device="cuda", generator=g)
     w = torch.randn((64, cin, 3, 3), device="cuda", generator=g) / (3 * cin ** 0.5)
     b = torch.randn(64, device="cuda", generator=g) * 0.1
     res = (torch.randn((B, 64, N, N), device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
            if use_res else None)
-    y = conv3x3(x, pack_conv3x3(w), b, relu, res)
+    # planar observation (cin 4, 8) / NHWC activation (cin 64)
+    xin = x.contiguous(memory_format=torch.channels_last) if cin == 64 else x.contiguous()
+    y = conv3x3(xin, pack_conv3x3(w), b, relu, res)
     torch.cuda.synchronize()
+    assert y.is_contiguous(memory_format=torch.channels_last)
     ref, bound = _ref(x, w, b, relu, res)
     err = (y.double() - ref).abs()
     assert bool((err <= 1e-5 * bound).all()), float((err / bound).max())
-    assert y.is_contiguous(memory_format=torch.channels_last)
 
 
 def test_leaf_resnet_matches_reference_forward():

@@ -14,7 +14,8 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 cin = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 256
 N = 20
-x = torch.randn(B, cin, N, N, device="cuda").contiguous(memory_format=torch.channels_last)
+x = torch.randn(B, cin, N, N, device="cuda")
+x = x.contiguous(memory_format=torch.channels_last) if cin == 64 else x.contiguous()
 w = pack_conv3x3(torch.randn(64, cin, 3, 3, device="cuda") * 0.05)
 b = torch.zeros(64, device="cuda")
 for _ in range(5):
