@@ -119,10 +119,21 @@ __global__ __launch_bounds__(256) void k_resnet_heads(const float* __restrict__ 
   __syncthreads();
   const int wave = t >> 6, l = t & 63;
   const int q0 = (NN * wave) / 4, q1 = (NN * (wave + 1)) / 4;
-  float acc = 0.f;
-#pragma unroll 4
-  for (int i = q0; i < q1; ++i) acc += w1t[(size_t)i * kHeadC + l] * vfeat[i];
-  part[wave * kHeadC + l] = acc;
+  // 10 independent loads in flight per lane, two accumulators (the fc1 sweep is latency-bound)
+  float acc0 = 0.f, acc1 = 0.f;
+  int i = q0;
+  for (; i + 10 <= q1; i += 10) {
+    float w[10];
+#pragma unroll
+    for (int u = 0; u < 10; ++u) w[u] = w1t[(size_t)(i + u) * kHeadC + l];
+#pragma unroll
+    for (int u = 0; u < 10; u += 2) {
+      acc0 += w[u] * vfeat[i + u];
+      acc1 += w[u + 1] * vfeat[i + u + 1];
+    }
+  }
+  for (; i < q1; ++i) acc0 += w1t[(size_t)i * kHeadC + l] * vfeat[i];
+  part[wave * kHeadC + l] = acc0 + acc1;
   __syncthreads();
   if (wave == 0) {
     const float h = fmaxf(((part[l] + part[kHeadC + l]) + (part[2 * kHeadC + l] + part[3 * kHeadC + l])) + b1[l], 0.0f);
