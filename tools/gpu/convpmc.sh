@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU step: bk_conv3x3 timing + PMC counters (one counter group per pass, kernel-trace only).
-# usage: tools_gpu_convpmc.sh [batch]
+# usage: tools/gpu/convpmc.sh [batch]
 set -o pipefail
 B=${1:-256}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
