@@ -78,28 +78,45 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     return sp, eng, done, elapsed, delta, ms
 
 
-def time_leaf_conv(sp, reps: int = 20):
-    """The dominant kernel of the self-play step, k_conv3x3 (a residual-block conv of the leaf
-    evaluator, 64 -> 64 channels at the leaf batch), timed live with HIP events on the stream it
-    is launched on. -> (ms per launch, algorithmic FLOP per launch) or None (no ResNet)."""
-    from ..nets import LeafResNet, conv3x3
+def time_leaf_conv(sp, reps: int = 5):
+    """The dominant kernel of the self-play step, k_conv3x3 (the 64 -> 64 residual-block convs of
+    the leaf evaluator at the leaf batch), timed live with HIP events on the stream it is
+    launched on: `reps` eager forwards of the leaf net on the search's last leaf batch, one event
+    pair around each residual-block conv launch (the graph-captured forward is the same kernel
+    sequence). -> (mean ms per launch, algorithmic FLOP per launch) or None (no HIP ResNet)."""
+    from .. import nets
+    from ..nets import LeafResNet
 
     model = getattr(sp.evaluator, "model", None)
     if not isinstance(model, LeafResNet) or not model.native or not len(model.f.blocks):
         return None
     G, N = sp.G, sp.eng.N
-    x = torch.relu(torch.randn((G, 64, N, N), device=sp.eng.device)).contiguous(memory_format=torch.channels_last)
-    w, b = model.w_0_1, model.f.blocks[0][0].bias
-    for _ in range(3):
-        conv3x3(x, w, b, True)
+    obs = sp.evaluator.static_obs
     st = torch.cuda.current_stream(sp.eng.device)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(reps):
-        conv3x3(x, w, b, True)
-    e1.record(st)
+    events = []
+    orig = nets.conv3x3
+
+    def timed(x, w, b, relu, residual=None):
+        if x.shape[1] != 64:  # the stem (planar observation input) is not a residual-block conv
+            return orig(x, w, b, relu, residual)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        y = orig(x, w, b, relu, residual)
+        e1.record(st)
+        events.append((e0, e1))
+        return y
+
+    nets.conv3x3 = timed
+    try:
+        model(obs)  # warm
+        events.clear()
+        for _ in range(reps):
+            model(obs)
+    finally:
+        nets.conv3x3 = orig
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps, 2.0 * G * N * N * 64 * 9 * 64
+    ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
+    return ms, 2.0 * G * N * N * 64 * 9 * 64
 
 
 def bench_selfplay(args, world, rank):
