@@ -412,9 +412,10 @@ def main():
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
-        if out["roofline"].get("kernel", "").startswith("k_conv3x3"):
-            # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv.json)
-            out["roofline"]["traffic"] = _pmc_traffic("k_conv3x3", args.games)
+        kname = out["roofline"].get("kernel", "").split(" ")[0]
+        if kname.startswith("k_conv3x3"):
+            # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)
+            out["roofline"]["traffic"] = _pmc_traffic(kname, args.games)
         if args.workload == "all":
             # env + search alone: the uninformed-MCTS opponent (DumbNet, compare_arena.py:87-95)
             _, _, dsims, dt, dctr, dms = run_selfplay("dumbnet", "fp32", args.games, args.sims, args.steps,

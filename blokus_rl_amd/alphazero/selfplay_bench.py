@@ -83,8 +83,12 @@ def time_leaf_conv(sp, reps: int = 5):
     the leaf evaluator at the leaf batch), timed live with HIP events on the stream it is
     launched on: `reps` eager forwards of the leaf net on the search's last leaf batch, one event
     pair around each residual-block conv launch (the graph-captured forward is the same kernel
-    sequence). -> (mean ms per launch, algorithmic FLOP per launch) or None (no HIP ResNet)."""
+    sequence). -> (mean ms per launch, FLOP per launch, form, direct-conv FLOP per launch) or None
+    (no HIP ResNet). FLOP = the arithmetic the kernel's MFMAs execute: for the Winograd
+    F(2x2,3x3) form 2*16*64*64 per 2x2 output tile (16 transform-domain GEMMs), for the direct
+    form 2*9*64*64 per output pixel."""
     from .. import nets
+    from ..engine import load_library
     from ..nets import LeafResNet
 
     model = getattr(sp.evaluator, "model", None)
@@ -116,7 +120,10 @@ def time_leaf_conv(sp, reps: int = 5):
         nets.conv3x3 = orig
     torch.cuda.synchronize()
     ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
-    return ms, 2.0 * G * N * N * 64 * 9 * 64
+    direct = 2.0 * G * N * N * 64 * 9 * 64
+    if load_library().bk_conv3x3_form(N, 64) == 1:
+        return ms, 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2, "winograd", direct
+    return ms, direct, "direct", direct
 
 
 def bench_selfplay(args, world, rank):
@@ -167,11 +174,14 @@ def bench_selfplay(args, world, rank):
         "engine_counters": delta,
     }
     if conv is not None:
-        cms, cflop = conv
-        out["roofline"] = {"bound": "mfma", "kernel": "k_conv3x3 (64->64, 3x3, fused bias+ReLU)",
+        cms, cflop, form, dflop = conv
+        kname = ("k_conv3x3_wino (Winograd F(2x2,3x3), f32 MFMA" if form == "winograd"
+                 else "k_conv3x3 (direct, f32 MFMA") + ", 64->64, fused bias+ReLU)"
+        out["roofline"] = {"bound": "mfma", "kernel": kname,
                            "achieved": cflop / (cms * 1e-3) / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
                            "frac": cflop / (cms * 1e-3) / FP32_PEAK, "traffic": None, "kernel_ms": cms,
                            "flop_per_launch": cflop, "units_per_launch": G,
+                           "direct_conv_equiv_tflops": dflop / (cms * 1e-3) / 1e12,
                            "launches_per_sim_step": 10, "share_of_sim_step": 10 * cms / (elapsed / steps_sim * 1e3)}
     else:
         out["roofline"] = out["search_roofline"]

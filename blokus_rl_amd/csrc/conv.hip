@@ -28,6 +28,7 @@
 #include "../../include/blokus_engine.h"
 #include "ctx.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace bk {
@@ -263,6 +264,242 @@ int launch_conv(const float* x, const f32x4* wp, const float* b, const float* r,
   return launch_check("k_conv3x3");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Winograd F(2x2, 3x3) form for CIN = 64 and even N (the 20x20 self-play net): all arithmetic
+// f32 (the f32 MFMA is an exact fmaf chain), 2.25x fewer multiplies than the direct form.
+// Each output 2x2 tile t (B * (N/2)^2 of them) reads its 4x4 input window d (zero padded), and
+//   y_t = A^T [ sum_cin U[cin] (.) (B^T d_cin B) ] A,   U = G g G^T (host, fp64 -> f32),
+// i.e. 16 independent GEMMs (one per transform position p = 4i + j) of [tiles x 64] x [64 x 64].
+// Mapping: a wave owns 16 tiles (MFMA columns) x KB blocks of 16 output channels (MFMA rows) x
+// all 16 positions = 16 KB accumulators. At k-step s lane (g = l>>4, m = l&15) takes channel
+// 16g + s of tile m's 16 window pixels (float4 loads: 4 steps each), transforms them in
+// registers (32 adds: the B operands of all 16 positions at once); the A operands (U) come from
+// LDS (conflict-free ds_read_b32, 256 B per (block, p, s)). Step s's MFMAs are interleaved with
+// step s+1's LDS reads and transform. After the last step each lane holds all 16 positions of
+// channels 4g..4g+3 (of each block) of its own tile: the output transform, bias, residual and
+// ReLU run in registers, one float4 store per output pixel and block. The workgroup (one per
+// CU) holds U for its 32-channel half (131 KB of LDS); blocks b and b + 8 sit on the same XCD
+// with opposite halves, and each XCD takes a contiguous eighth of the tile groups, so both
+// halves of a window are fetched into one L2.
+//   KB = 1: 8 waves (2 per SIMD, 256 registers), waves w and w^1 the two blocks of a group.
+//   KB = 2: 4 waves (1 per SIMD, 512 registers), a wave both blocks.
+#ifndef BK_WINO_KB
+#define BK_WINO_KB 1
+#endif
+constexpr int kWinoKB = BK_WINO_KB;
+#ifndef BK_WINO_STAMP
+#define BK_WINO_STAMP 0  // timing diagnostics only: per-wave s_memtime stamps (bk_wino_stamps)
+#endif
+#if BK_WINO_STAMP
+constexpr int kStampPerWave = 32;
+__device__ unsigned long long g_wino_stamps[256 * 8 * kStampPerWave];
+#define WSTAMP(i)                                                                                      \
+  do {                                                                                                 \
+    if (l == 0 && (i) < kStampPerWave)                                                                 \
+      g_wino_stamps[(blockIdx.x * 8 + wave) * kStampPerWave + (i)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#else
+#define WSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+constexpr int kWinoThreads = kWinoKB == 1 ? 512 : 256;
+constexpr int kWinoHalf = 2 * 16 * 16 * kWave;  // floats of U per 32-channel half: [2 blk][16 p][16 s][64]
+
+template <int KB, bool RELU, bool RES>
+__global__ __launch_bounds__(KB == 1 ? 512 : 256, 1) void k_conv3x3_wino(const float* __restrict__ x,
+                                                                         const float* __restrict__ uw,
+                                                                         const float* __restrict__ bias,
+                                                                         const float* __restrict__ res,
+                                                                         float* __restrict__ y, int N, int tiles) {
+  constexpr int kThreads = KB == 1 ? 512 : 256;
+  constexpr int kSlots = 4;            // groups in flight per workgroup
+  constexpr int NBUF = KB == 1 ? 1 : 2;  // float4 window buffers (A prefetch depth)
+  extern __shared__ __attribute__((aligned(16))) float u_lds[];  // [2 blk][16 p][16 s][64 lanes]
+  const int half = (blockIdx.x >> 3) & 1, xcd = blockIdx.x & 7;
+  const int cu = blockIdx.x >> 4, ncu = gridDim.x >> 4;
+  const int groups = (tiles + 15) >> 4;
+  const int g_begin = (int)((int64_t)groups * xcd / 8), g_end = (int)((int64_t)groups * (xcd + 1) / 8);
+  const int range = g_end - g_begin;
+  const int c_lo = g_begin + (int)((int64_t)range * cu / ncu), c_hi = g_begin + (int)((int64_t)range * (cu + 1) / ncu);
+  if (c_lo == c_hi) return;
+  {
+    const float4* src = reinterpret_cast<const float4*>(uw + (size_t)half * kWinoHalf);
+    float4* dst = reinterpret_cast<float4*>(u_lds);
+    for (int i = threadIdx.x; i < kWinoHalf / 4; i += kThreads) dst[i] = src[i];
+  }
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  WSTAMP(0);
+  __syncthreads();
+  WSTAMP(1);
+  const int m = l & 15, g = l >> 4;
+  const int kb0 = KB == 1 ? (wave & 1) : 0, slot = KB == 1 ? (wave >> 1) : wave;
+  const int T2 = N >> 1, tpb = T2 * T2;
+  const float* ub = u_lds + kb0 * (16 * 16 * kWave) + l;
+  float bias_k[KB][4];
+#pragma unroll
+  for (int k = 0; k < KB; ++k)
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) bias_k[k][vv] = bias[32 * half + 16 * (kb0 + k) + 4 * g + vv];
+  // the input through a buffer descriptor: 32-bit offsets, and out-of-range reads return 0 —
+  // a window pixel off the board (zero padding) or past the last tile gets an offset beyond the
+  // buffer, so padding costs nothing in the inner loop
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, tiles * 1024, 0x00020000);
+  constexpr unsigned kOut = 0x7fff0000u;
+  // byte offsets of this lane's tile (MFMA column m) window: 16 pixels, channel 16g
+  auto window = [&](int grp, unsigned (&off)[16]) {
+    const int tile = grp * 16 + m;
+    const bool tv = tile < tiles;
+    const int b = tv ? tile / tpb : 0, r = tv ? tile - b * tpb : 0;
+    const int ty = r / T2, tx = r - ty * T2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int yy = 2 * ty - 1 + i, xx = 2 * tx - 1 + j;
+        const bool v = tv && yy >= 0 && yy < N && xx >= 0 && xx < N;
+        off[4 * i + j] = v ? (unsigned)(((b * N + yy) * N + xx) * 256 + 64 * g) : kOut;
+      }
+  };
+  auto ld = [&](unsigned o) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
+  };
+  unsigned off[16];
+  f32x4 raw[NBUF][16];
+  int grp = c_lo + slot;
+  if (grp < c_hi) {
+    window(grp, off);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) raw[0][q] = ld(off[q]);
+  }
+  int task = 0;
+  for (; grp < c_hi; grp += kSlots, ++task) {
+    WSTAMP(2 + 3 * task);
+    f32x4 acc[KB][16];
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+#pragma unroll
+      for (int p = 0; p < 16; ++p) acc[k][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bw[2][16 * KB];
+#pragma unroll
+    for (int kp = 0; kp < 16 * KB; ++kp) bw[0][kp] = ub[(kp * 16) * kWave];
+    const int nxt = grp + kSlots;
+    // A loads of quad qd (channels 16g + 4qd .. +3) into buf, or the next group's first quad
+    auto load_quad = [&](int qd, int buf) {
+      if (qd < 4) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) raw[buf][q] = ld(off[q] + 16 * qd);
+      } else if (nxt < c_hi) {
+        unsigned offn[16];
+        window(nxt, offn);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) raw[buf][q] = ld(offn[q]);
+      }
+    };
+    // B^T d B of k-step s: the B operands of its 16 positions
+    auto transform = [&](int s, float (&v)[16]) {
+      float d[16], t[16];
+      const int r = s & 3;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) d[q] = raw[NBUF == 2 ? (s >> 2) & 1 : 0][q][r];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[0 + j] = d[0 + j] - d[8 + j];
+        t[4 + j] = d[4 + j] + d[8 + j];
+        t[8 + j] = d[8 + j] - d[4 + j];
+        t[12 + j] = d[4 + j] - d[12 + j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[4 * i + 0] = t[4 * i + 0] - t[4 * i + 2];
+        v[4 * i + 1] = t[4 * i + 1] + t[4 * i + 2];
+        v[4 * i + 2] = t[4 * i + 2] - t[4 * i + 1];
+        v[4 * i + 3] = t[4 * i + 1] - t[4 * i + 3];
+      }
+    };
+    float vc[16];
+    transform(0, vc);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (NBUF == 2 && (s & 3) == 0) load_quad((s >> 2) + 1, ((s >> 2) + 1) & 1);
+      float vn[16];
+      if (s + 1 < 16) {
+#pragma unroll
+        for (int kp = 0; kp < 16 * KB; ++kp) bw[(s + 1) & 1][kp] = ub[(kp * 16 + s + 1) * kWave];
+        transform(s + 1, vn);
+        // single buffer: the quad's last transform done -> refill it with the next quad
+        if (NBUF == 1 && ((s + 1) & 3) == 3) load_quad(((s + 1) >> 2) + 1, 0);
+      }
+      // U as the A operand (rows = output channels), the window as B (columns = tiles):
+      // D[channel 4g + vv][tile m]
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+          acc[k][p] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[s & 1][k * 16 + p], vc[p], acc[k][p], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");  // keep each step's loads in its step (no hoisting across steps)
+      if (s + 1 < 16) {
+#pragma unroll
+        for (int p = 0; p < 16; ++p) vc[p] = vn[p];
+      }
+    }
+    WSTAMP(3 + 3 * task);
+    // A^T M A for (tile m; channels 32h + 16(kb0 + k) + 4g + vv) + bias (+ residual), ReLU
+    const int tile = grp * 16 + m;
+    if (tile < tiles) {
+      const int ob = tile / tpb, orr = tile - ob * tpb;
+      const int oy = 2 * (orr / T2), ox = 2 * (orr - (orr / T2) * T2);
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        float yv[4][4];  // [pixel 2i + j][vv]
+#pragma unroll
+        for (int vv = 0; vv < 4; ++vv) {
+          float u2[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            u2[j] = acc[k][j][vv] + acc[k][4 + j][vv] + acc[k][8 + j][vv];
+            u2[4 + j] = acc[k][4 + j][vv] - acc[k][8 + j][vv] - acc[k][12 + j][vv];
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            yv[2 * i][vv] = u2[4 * i + 0] + u2[4 * i + 1] + u2[4 * i + 2] + bias_k[k][vv];
+            yv[2 * i + 1][vv] = u2[4 * i + 1] - u2[4 * i + 2] - u2[4 * i + 3] + bias_k[k][vv];
+          }
+        }
+#pragma unroll
+        for (int px = 0; px < 4; ++px) {
+          const size_t o =
+              ((size_t)(ob * N + oy + (px >> 1)) * N + ox + (px & 1)) * 64 + 32 * half + 16 * (kb0 + k) + 4 * g;
+          float4 out = make_float4(yv[px][0], yv[px][1], yv[px][2], yv[px][3]);
+          if (RES) {
+            const float4 rr = *reinterpret_cast<const float4*>(res + o);
+            out.x += rr.x;
+            out.y += rr.y;
+            out.z += rr.z;
+            out.w += rr.w;
+          }
+          if (RELU) {
+            out.x = fmaxf(out.x, 0.0f);
+            out.y = fmaxf(out.y, 0.0f);
+            out.z = fmaxf(out.z, 0.0f);
+            out.w = fmaxf(out.w, 0.0f);
+          }
+          *reinterpret_cast<float4*>(y + o) = out;
+        }
+      }
+    }
+    if (nxt < c_hi) window(nxt, off);
+    WSTAMP(4 + 3 * task);
+  }
+}
+
+// BK_CONV_DIRECT=1 forces the direct form for every shape (tests compare the two)
+bool direct_only() {
+  const char* e = getenv("BK_CONV_DIRECT");
+  return e && *e && *e != '0';
+}
+
 }  // namespace
 }  // namespace bk
 
@@ -270,7 +507,23 @@ using namespace bk;
 
 extern "C" {
 
-int bk_conv3x3_packed_floats(int cin) { return (cin == 4 || cin == 8 || cin == 64) ? 9 * cin * kCout : -1; }
+#if BK_WINO_STAMP
+// diagnostics build only: copy the per-wave stamps [256 blocks][8 waves][32] to host memory
+int bk_wino_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wino_stamps), sizeof(g_wino_stamps)) == hipSuccess ? 0 : -1;
+}
+int bk_wino_stamps_clear() {
+  static unsigned long long zeros[256 * 8 * kStampPerWave];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wino_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int bk_conv3x3_packed_floats(int cin) {
+  // cin 64: the direct form's 9*64*64 operands, then the Winograd form's U (2 halves)
+  return (cin == 4 || cin == 8) ? 9 * cin * kCout : cin == 64 ? 9 * 64 * kCout + 2 * kWinoHalf : -1;
+}
+
+int bk_conv3x3_form(int N, int cin) { return cin == 64 && N % 2 == 0 && !direct_only() ? 1 : 0; }
 
 int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, const float* bias, const float* residual,
                int relu, float* y, void* stream) {
@@ -302,6 +555,36 @@ int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, cons
                       "hipFuncSetAttribute") != BK_OK)
           return BK_EHIP;
       attr_set = true;
+    }
+    if (bk_conv3x3_form(N, cin) == 1) {
+      static bool wattr = false;
+      const int lds = (int)(sizeof(float) * kWinoHalf);
+      if (!wattr) {
+        const void* fns[4] = {(const void*)k_conv3x3_wino<kWinoKB, true, true>, (const void*)k_conv3x3_wino<kWinoKB, true, false>,
+                              (const void*)k_conv3x3_wino<kWinoKB, false, true>, (const void*)k_conv3x3_wino<kWinoKB, false, false>};
+        for (const void* fn : fns)
+          if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                        "hipFuncSetAttribute") != BK_OK)
+            return BK_EHIP;
+        wattr = true;
+      }
+      BK_REQUIRE(total * 64 < (1ll << 31), "bk_conv3x3: batch too large");
+      const float* uw = wpacked + 9 * 64 * kCout;
+      const int tiles = (int)(total / 4);
+      const int g = blocks >= 16 ? blocks / 16 * 16 : 16;
+      if (relu && residual)
+        hipLaunchKernelGGL((k_conv3x3_wino<kWinoKB, true, true>), dim3(g), dim3(kWinoThreads), lds, s, x, uw, bias, residual, y, N,
+                           tiles);
+      else if (relu)
+        hipLaunchKernelGGL((k_conv3x3_wino<kWinoKB, true, false>), dim3(g), dim3(kWinoThreads), lds, s, x, uw, bias, residual, y,
+                           N, tiles);
+      else if (residual)
+        hipLaunchKernelGGL((k_conv3x3_wino<kWinoKB, false, true>), dim3(g), dim3(kWinoThreads), lds, s, x, uw, bias, residual, y,
+                           N, tiles);
+      else
+        hipLaunchKernelGGL((k_conv3x3_wino<kWinoKB, false, false>), dim3(g), dim3(kWinoThreads), lds, s, x, uw, bias, residual,
+                           y, N, tiles);
+      return launch_check("k_conv3x3_wino");
     }
     return launch_conv<64, 4>(x, wp, bias, residual, y, N, (int)total, relu, s, blocks);
   }

@@ -175,7 +175,8 @@ def _bias_act(x: torch.Tensor, bias: torch.Tensor, relu: bool, residual: torch.T
 
 
 def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
-    """[64, cin, 3, 3] weights -> bk_conv3x3's operand order: flat [9][cin/4][64 lanes][4 blocks],
+    """[64, cin, 3, 3] weights -> bk_conv3x3's operand order: flat [9][cin/4][64 lanes][4 blocks]
+    (cin 64: followed by pack_winograd(w) for the Winograd form used at even N),
     element (tap, s, l, j) = w[16j + (l & 15), cin(s, l >> 4), tap // 3, tap % 3] with
     cin(s, g) = 4*VEC*(s // VEC) + VEC*g + s % VEC, VEC = 4 (cin % 16 == 0), 2 (cin 8), 1 (cin 4)."""
     cout, cin = w.shape[0], w.shape[1]
@@ -188,8 +189,30 @@ def pack_conv3x3(w: torch.Tensor) -> torch.Tensor:
     j = torch.arange(4, device=dev).view(1, 1, 1, 4)
     ci = 4 * vec * (s // vec) + vec * (lane >> 4) + s % vec
     co = 16 * j + (lane & 15)
-    out = w.float()[co, ci, tap // 3, tap % 3]
-    return out.contiguous().view(-1)
+    out = w.float()[co, ci, tap // 3, tap % 3].contiguous().view(-1)
+    if cin != 64:
+        return out
+    return torch.cat([out, pack_winograd(w)])
+
+
+_WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+def pack_winograd(w: torch.Tensor) -> torch.Tensor:
+    """[64, 64, 3, 3] -> the Winograd F(2x2,3x3) form's U = G w G^T (computed in fp64, stored f32) in
+    k_conv3x3_wino's LDS order: flat [2 halves h][2 blocks k][16 positions p][16 k-steps s][64 lanes],
+    element = U[32h + 16k + (l & 15), 16 * (l >> 4) + s, p // 4, p % 4]."""
+    assert w.shape == (64, 64, 3, 3)
+    G = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
+    U = torch.einsum("ik,ockl,jl->ocij", G, w.double(), G).reshape(64, 64, 16)  # [cout][cin][p]
+    dev = w.device
+    h = torch.arange(2, device=dev).view(2, 1, 1, 1, 1)
+    k = torch.arange(2, device=dev).view(1, 2, 1, 1, 1)
+    pos = torch.arange(16, device=dev).view(1, 1, 16, 1, 1)
+    st = torch.arange(16, device=dev).view(1, 1, 1, 16, 1)
+    lane = torch.arange(64, device=dev).view(1, 1, 1, 1, 64)
+    out = U[32 * h + 16 * k + (lane & 15), 16 * (lane >> 4) + st, pos]
+    return out.float().contiguous().view(-1)
 
 
 def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bool,
@@ -204,10 +227,12 @@ def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bo
         assert x.is_contiguous(memory_format=torch.channels_last)
     else:
         assert x.is_contiguous()
+    lib = load_library()
+    assert wpacked.dtype == torch.float32 and wpacked.numel() == lib.bk_conv3x3_packed_floats(cin)
     y = torch.empty((B, 64, N, N), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
     if residual is not None:
         assert residual.is_contiguous(memory_format=torch.channels_last) and residual.shape == y.shape
-    _check(load_library().bk_conv3x3(ctypes.c_void_p(x.data_ptr()), B, N, cin, _ptr(wpacked), _ptr(bias),
+    _check(lib.bk_conv3x3(ctypes.c_void_p(x.data_ptr()), B, N, cin, _ptr(wpacked), _ptr(bias),
                                      None if residual is None else ctypes.c_void_p(residual.data_ptr()), int(relu),
                                      ctypes.c_void_p(y.data_ptr()), _stream(x.device)))
     return y

@@ -244,9 +244,13 @@ int bk_bias_act(float* x, int64_t n, int C, const float* bias, const float* resi
 /* 3x3 convolution, stride 1, zero padding 1, 64 output channels, with the fused epilogue
  * y = act(conv(x) + bias (+ residual)), f32. Layouts: cin 64 input, y and residual are NHWC
  * [B][N][N][64]; cin 4 or 8 input is planar [B][cin][N][N] (the observation). wpacked: the 9*cin*64 weights in the kernel's MFMA operand order
- * (blokus_rl_amd/nets.py pack_conv3x3 documents it); bk_conv3x3_packed_floats(cin) = its length.
+ * (blokus_rl_amd/nets.py pack_conv3x3 documents it; cin 64 appends the Winograd F(2x2,3x3)
+ * transformed weights, used at even N); bk_conv3x3_packed_floats(cin) = its length.
+ * BK_CONV_DIRECT=1 in the environment forces the direct form for every shape.
  * Replaces conv + BN (folded) + ReLU (+ residual add) of blokus_nnet.py:135-146. */
 int bk_conv3x3_packed_floats(int cin);
+/* Which form bk_conv3x3 runs for (N, cin): 1 = Winograd F(2x2,3x3) (cin 64, even N), 0 = direct. */
+int bk_conv3x3_form(int N, int cin);
 /* The ResNet heads (blokus_nnet.py:146-150, BN folded) from the tower output x [B][NN][64] NHWC:
  * pf[B][2*NN] = relu(1x1 conv 64->2 + bp) flattened channel-major (the policy Linear's input),
  * v[B][P] = tanh(W2 relu(W1 relu(1x1 conv 64->1 + bv) + b1) + b2); wp [2][64], wv [64],

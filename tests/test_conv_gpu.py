@@ -20,7 +20,7 @@ def _ref(x, w, b, relu, res):
 
 
 @pytest.mark.parametrize("B,N,cin", [(256, 20, 64), (3, 20, 64), (1, 20, 8), (256, 20, 8), (5, 7, 4), (7, 7, 64),
-                                     (33, 20, 64)])
+                                     (33, 20, 64), (1, 20, 64), (300, 20, 64), (9, 8, 64), (3, 2, 64), (2, 14, 64)])
 @pytest.mark.parametrize("relu,use_res", [(True, False), (False, False), (True, True), (False, True)])
 def test_conv3x3_matches_torch(B, N, cin, relu, use_res):
     from blokus_rl_amd.nets import conv3x3, pack_conv3x3
@@ -39,6 +39,29 @@ def test_conv3x3_matches_torch(B, N, cin, relu, use_res):
     ref, bound = _ref(x, w, b, relu, res)
     err = (y.double() - ref).abs()
     assert bool((err <= 1e-5 * bound).all()), float((err / bound).max())
+
+
+@pytest.mark.parametrize("B", [1, 37, 256])
+def test_winograd_and_direct_forms_agree(B, monkeypatch):
+    """Even N runs the Winograd F(2x2,3x3) form, BK_CONV_DIRECT=1 the direct one: both f32,
+    both within the f32 bound of the fp64 convolution, and close to each other."""
+    from blokus_rl_amd.nets import conv3x3, pack_conv3x3
+
+    g = torch.Generator(device="cuda").manual_seed(B)
+    x = torch.relu(torch.randn((B, 64, 20, 20), device="cuda", generator=g))
+    w = torch.randn((64, 64, 3, 3), device="cuda", generator=g) / 24
+    b = torch.randn(64, device="cuda", generator=g) * 0.1
+    wp = pack_conv3x3(w)
+    xin = x.contiguous(memory_format=torch.channels_last)
+    y_w = conv3x3(xin, wp, b, True)
+    monkeypatch.setenv("BK_CONV_DIRECT", "1")
+    y_d = conv3x3(xin, wp, b, True)
+    torch.cuda.synchronize()
+    ref, bound = _ref(x, w, b, True, None)
+    for y in (y_w, y_d):
+        assert bool(((y.double() - ref).abs() <= 1e-5 * bound).all())
+    assert bool(((y_w.double() - y_d.double()).abs() <= 2e-5 * bound).all())
+    assert not torch.equal(y_w, y_d)  # two different kernels really ran
 
 
 def test_leaf_resnet_matches_reference_forward():
