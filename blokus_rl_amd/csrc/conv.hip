@@ -35,6 +35,7 @@ namespace bk {
 namespace {
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 constexpr int kCout = 64;
 #ifndef BK_CONV_THREADS
 #define BK_CONV_THREADS 768
@@ -298,9 +299,16 @@ __device__ unsigned long long g_wino_stamps[256 * 8 * kStampPerWave];
     if (l == 0 && (i) < kStampPerWave)                                                                 \
       g_wino_stamps[(blockIdx.x * 8 + wave) * kStampPerWave + (i)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
+#define W2STAMP(i, v)                                                                         \
+  do {                                                                                        \
+    if (l == 0 && (i) < kStampPerWave) g_wino_stamps[(blockIdx.x * 8 + wave) * kStampPerWave + (i)] = (v); \
+  } while (0)
 #else
 #define WSTAMP(i) \
   do {            \
+  } while (0)
+#define W2STAMP(i, v) \
+  do {                \
   } while (0)
 #endif
 constexpr int kWinoThreads = kWinoKB == 1 ? 512 : 256;
@@ -494,10 +502,256 @@ __global__ __launch_bounds__(KB == 1 ? 512 : 256, 1) void k_conv3x3_wino(const f
   }
 }
 
-// BK_CONV_DIRECT=1 forces the direct form for every shape (tests compare the two)
+// ---------------------------------------------------------------------------------------------
+// Winograd F(2x2, 3x3), form 2 (the default): the same arithmetic as k_conv3x3_wino, but the
+// transformed weights U stay in REGISTERS and the transformed input windows V go through LDS,
+// so every input window is loaded and transformed once per launch (form 1 does it 4x: two
+// channel halves on two CUs x two waves) and one CU covers all 64 output channels.
+//  * One 256-thread workgroup per CU (4 waves, 1 per SIMD). Wave kb holds U for output channels
+//    16kb..16kb+15 in AGPRs: per lane the A operands of all 16 positions x 16 k-steps (256
+//    registers), loaded once per launch (64 KB per wave, L2-resident).
+//  * Work unit = a group of 16 output tiles (one MFMA column each); the 8 XCDs take contiguous
+//    eighths of the groups, each CU a contiguous run of them (its windows share board rows in
+//    L1/L2). Per group the CU's 256 threads each transform one (tile, 4-channel quad): 16
+//    float4 window loads (buffer loads; off-board and past-the-end pixels read 0), B^T d B in
+//    registers on channel pairs (v_pk_add_f32), 16 ds_write_b128 into V[s][p][t][4 channels].
+//  * MFMA loop (per group, per wave): 16 k-steps x 16 positions of v_mfma_f32_16x16x4_f32,
+//    A = U straight from AGPRs (inline asm), B = V (16 conflict-free ds_read_b32 per step, one
+//    step ahead), accumulators in VGPRs; the bias is the initial accumulator of position (1,1),
+//    which the output transform adds to all four pixels of a tile.
+//  * f32 MFMAs run on the SIMD's vector ALUs: a VALU instruction beside them is not hidden, and
+//    each switch between MFMA and VALU costs ~10 cycles (measured, tools/probe/mfma_fill.hip).
+//    So the loop body is MFMAs and LDS reads only; the VALU work comes in three batches per
+//    group, all on packed pairs: the window offsets (step 0), the next group's input transform
+//    (after step 7; its loads were issued at step 0) and the output transform epilogue.
+//  * V is double-buffered in LDS (2 x 64 KB): one barrier per group.
+// packed f32 add / subtract (v_pk_add_f32, with the second operand negated for a - b: the same
+// IEEE result as a scalar subtraction); the compiler splits a <2 x float> fsub into two VALU ops
+__device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+constexpr int kW2Threads = 256;
+constexpr int kW2UFloats = 4 * 64 * kWave * 4;  // [4 kb][64 q][64 lanes][4]: (s, p) = divmod(4q + e, 16)
+constexpr int kW2VBuf = 16 * 16 * 16 * 4;      // floats per V buffer: [16 s][16 p][16 t][4 g]
+
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __restrict__ x,
+                                                                 const float* __restrict__ u2,
+                                                                 const float* __restrict__ bias,
+                                                                 const float* __restrict__ res,
+                                                                 float* __restrict__ y, int N, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) float v_lds[];  // [2 buf][16 s][16 p][16 t][4 g]
+  const int xcd = blockIdx.x & 7, cu = blockIdx.x >> 3, ncu = gridDim.x >> 3;
+  const int groups = (tiles + 15) >> 4;
+  const int g_begin = (int)((int64_t)groups * xcd / 8), g_end = (int)((int64_t)groups * (xcd + 1) / 8);
+  const int range = g_end - g_begin;
+  const int c_lo = g_begin + (int)((int64_t)range * cu / ncu), c_hi = g_begin + (int)((int64_t)range * (cu + 1) / ncu);
+  if (c_lo == c_hi) return;
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  W2STAMP(0, __builtin_amdgcn_s_memtime());
+  W2STAMP(30, __builtin_amdgcn_s_memrealtime());
+  const int T2 = N >> 1, tpb = T2 * T2;
+  // transform role: tile tt of the group, k-step (channel quad) sq
+  const int tt = l & 15, sq = (wave << 2) | (l >> 4);
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, tiles * 1024, 0x00020000);
+  constexpr unsigned kOut = 0x7fff0000u;
+  // window offsets, branch-free: a row or column off the board (or a tile past the end) gets a
+  // base of kOut, so the sum lands beyond the buffer and the load returns 0. Also returns the
+  // group's output pixel index for lane l's tile (the epilogue's, -1 past the end).
+  auto window = [&](int grp, unsigned (&off)[16]) {
+    const unsigned tile = (unsigned)(grp * 16 + tt);
+    const bool tv = tile < (unsigned)tiles;
+    const unsigned b = tile / (unsigned)tpb, r = tile - b * (unsigned)tpb;
+    const int ty = (int)(r / (unsigned)T2), tx = (int)r - ty * T2;
+    const int rbase = ((int)b * N + 2 * ty - 1) * N * 256 + 16 * sq, cbase = (2 * tx - 1) * 256;
+    unsigned rb[4], cb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int yy = 2 * ty - 1 + i, xx = 2 * tx - 1 + i;
+      rb[i] = tv && yy >= 0 && yy < N ? (unsigned)(rbase + i * N * 256) : kOut;
+      cb[i] = xx >= 0 && xx < N ? (unsigned)(cbase + i * 256) : kOut;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) off[4 * i + j] = rb[i] + cb[j];
+  };
+  auto out_pixel = [&](int grp) {  // top-left output pixel of lane l's tile in group grp
+    const unsigned tile = (unsigned)(grp * 16 + (l & 15));
+    const unsigned b = tile / (unsigned)tpb, r = tile - b * (unsigned)tpb;
+    const int ty = (int)(r / (unsigned)T2), tx = (int)r - ty * T2;
+    return tile < (unsigned)tiles ? ((int)b * N + 2 * ty) * N + 2 * tx : -1;
+  };
+  auto ld = [&](unsigned o) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0)); };
+  // B^T d B of this thread's 4 channels as two packed pairs h -> V[buf][sq][p][tt][2h, 2h+1], in 8
+  // parts k = (h, i): row i of the 4x4 result, t_i = (B^T d)_i from two window rows, v_i = t_i B
+  auto transform_part = [&](const f32x4 (&raw)[16], int buf, int k) {
+    const int h = k >> 2, i = k & 3;
+    float* dst = v_lds + buf * kW2VBuf + sq * 1024 + tt * 4 + 2 * h;
+    auto d = [&](int q) { return h ? raw[q].zw : raw[q].xy; };
+    f32x2 t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i == 0) t[j] = pk_sub(d(j), d(8 + j));
+      else if (i == 1) t[j] = pk_add(d(4 + j), d(8 + j));
+      else if (i == 2) t[j] = pk_sub(d(8 + j), d(4 + j));
+      else t[j] = pk_sub(d(4 + j), d(12 + j));
+    }
+    *reinterpret_cast<f32x2*>(dst + (4 * i + 0) * 64) = pk_sub(t[0], t[2]);
+    *reinterpret_cast<f32x2*>(dst + (4 * i + 1) * 64) = pk_add(t[1], t[2]);
+    *reinterpret_cast<f32x2*>(dst + (4 * i + 2) * 64) = pk_sub(t[2], t[1]);
+    *reinterpret_cast<f32x2*>(dst + (4 * i + 3) * 64) = pk_sub(t[1], t[3]);
+  };
+  // prologue: the first two groups' windows and the bias, then this wave's U (AGPRs) for k-steps
+  // 0 and 1, ur[4s + p/4][p%4] = U[16 wave + (l & 15)][4s + (l >> 4)][p]. The first group's MFMA
+  // loop (a peeled copy of the group body, whose window loads are these) loads U two k-steps
+  // ahead and waits for each k-step's U as it arrives: U streams in under its MFMAs.
+  f32x4 ur[64];
+  f32x4 raw[16];
+  unsigned off[16];
+  f32x4 bias4;
+  const f32x4* usrc = reinterpret_cast<const f32x4*>(u2) + (size_t)wave * 64 * kWave + l;
+  {
+    f32x4 raw0[16];
+    window(c_lo, off);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) raw0[q] = ld(off[q]);
+    window(c_lo + 1 < c_hi ? c_lo + 1 : c_lo, off);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) raw[q] = ld(off[q]);
+    // the bias as the initial accumulator of position (1,1) (p = 5): the output transform adds
+    // M(1,1) to all four pixels of a tile
+    bias4 = *reinterpret_cast<const f32x4*>(bias + 16 * wave + 4 * (l >> 4));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // k-steps 0 and 1; the peeled group loads the rest
+      ur[q] = usrc[q * kWave];
+      __builtin_amdgcn_sched_barrier(0);  // keep k-step order: the peeled group waits step by step
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) transform_part(raw0, 0, k);
+  }
+  W2STAMP(28, __builtin_amdgcn_s_memtime());
+  __syncthreads();
+  W2STAMP(1, __builtin_amdgcn_s_memtime());
+  const float* vrd = v_lds + (l & 15) * 4 + (l >> 4);  // lane (g, t) reads V[.][s][p][t][g]
+  int opix = out_pixel(c_lo);
+  // one group: 16 k-steps of 16 MFMAs (A = U from AGPRs, B = V from LDS one step ahead); the next
+  // group's window loads go out over steps 0-3 (offsets at step 0) and its transform runs in 8
+  // parts over steps 8-15; then the output transform and one barrier. The last group re-reads
+  // its own window into the idle V buffer, so loads and transforms stay unconditional.
+  auto run_group = [&](int grp, int buf, auto first) {
+    W2STAMP(2 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
+    const int nxt = grp + 1 < c_hi ? grp + 1 : grp;
+    f32x4 acc[16];
+    const float* vsrc = vrd + buf * kW2VBuf;
+    float vb[2][16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) vb[0][p] = vsrc[p * 64];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s == 0 && !decltype(first)::value) window(nxt, off);
+      if (s < 4 && !decltype(first)::value) {
+#pragma unroll
+        for (int q = 4 * s; q < 4 * s + 4; ++q) raw[q] = ld(off[q]);
+      }
+      if (decltype(first)::value && s + 2 < 16) {  // U of k-step s + 2, in order
+#pragma unroll
+        for (int q = 4 * (s + 2); q < 4 * (s + 2) + 4; ++q) {
+          ur[q] = usrc[q * kWave];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (!decltype(first)::value && grp - c_lo == 2 && (s == 4 || s == 8 || s == 12))
+        W2STAMP(22 + s / 4, __builtin_amdgcn_s_memtime());
+      if (s + 1 < 16) {  // B operands of the next k-step, before any VALU work of this one
+#pragma unroll
+        for (int p = 0; p < 16; ++p) vb[(s + 1) & 1][p] = vsrc[((s + 1) * 16 + p) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (s >= 8) transform_part(raw, buf ^ 1, s - 8);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        const float ua = ur[4 * s + (p >> 2)][p & 3];
+        const float vv = vb[s & 1][p];
+        if (s == 0 && p == 5)
+          asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %3" : "=&v"(acc[p]) : "a"(ua), "v"(vv), "v"(bias4));
+        else if (s == 0)
+          asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(acc[p]) : "a"(ua), "v"(vv));
+        else
+          asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc[p]) : "a"(ua), "v"(vv));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the accumulators are written by MFMAs the compiler cannot see: wait out the XDL
+    // write -> VALU read latency before the epilogue reads them
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    W2STAMP(3 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
+    // A^T M A for (lane l's tile; channels 16 wave + 4 (l >> 4) + 0..3) on packed channel pairs
+    if (opix >= 0) {
+      f32x2 yv[4][2];  // [pixel 2i + j][pair h]
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        auto m = [&](int q) { return h ? acc[q].zw : acc[q].xy; };
+        f32x2 u2v[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          u2v[j] = pk_add(pk_add(m(j), m(4 + j)), m(8 + j));
+          u2v[4 + j] = pk_sub(pk_sub(m(4 + j), m(8 + j)), m(12 + j));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          yv[2 * i][h] = pk_add(pk_add(u2v[4 * i + 0], u2v[4 * i + 1]), u2v[4 * i + 2]);
+          yv[2 * i + 1][h] = pk_sub(pk_sub(u2v[4 * i + 1], u2v[4 * i + 2]), u2v[4 * i + 3]);
+        }
+      }
+#pragma unroll
+      for (int px = 0; px < 4; ++px) {
+        const size_t o = (size_t)(opix + (px >> 1) * N + (px & 1)) * 64 + 16 * wave + 4 * (l >> 4);
+        f32x2 lo = yv[px][0], hi = yv[px][1];
+        if (RES) {
+          const f32x4 rr = *reinterpret_cast<const f32x4*>(res + o);
+          lo = pk_add(lo, rr.xy);
+          hi = pk_add(hi, rr.zw);
+        }
+        f32x4 out = f32x4{lo.x, lo.y, hi.x, hi.y};
+        if (RELU) {
+          out.x = fmaxf(out.x, 0.0f);
+          out.y = fmaxf(out.y, 0.0f);
+          out.z = fmaxf(out.z, 0.0f);
+          out.w = fmaxf(out.w, 0.0f);
+        }
+        *reinterpret_cast<f32x4*>(y + o) = out;
+      }
+    }
+    opix = out_pixel(nxt);
+    __syncthreads();  // V[buf ^ 1] complete for the next group; V[buf] free to be overwritten
+    W2STAMP(4 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
+  };
+  run_group(c_lo, 0, std::true_type{});  // peeled: its MFMAs wait for U k-step by k-step
+  int buf = 1;
+  for (int grp = c_lo + 1; grp < c_hi; ++grp, buf ^= 1) run_group(grp, buf, std::false_type{});
+  W2STAMP(29, __builtin_amdgcn_s_memtime());
+  W2STAMP(31, __builtin_amdgcn_s_memrealtime());
+}
+
+// BK_CONV_DIRECT=1 forces the direct form for every shape (tests compare the two);
+// BK_CONV_WINO=1 selects Winograd form 1 (k_conv3x3_wino) instead of form 2
 bool direct_only() {
   const char* e = getenv("BK_CONV_DIRECT");
   return e && *e && *e != '0';
+}
+bool wino_form1() {
+  const char* e = getenv("BK_CONV_WINO");
+  return e && *e == '1';
 }
 
 }  // namespace
@@ -520,7 +774,7 @@ int bk_wino_stamps_clear() {
 
 int bk_conv3x3_packed_floats(int cin) {
   // cin 64: the direct form's 9*64*64 operands, then the Winograd form's U (2 halves)
-  return (cin == 4 || cin == 8) ? 9 * cin * kCout : cin == 64 ? 9 * 64 * kCout + 2 * kWinoHalf : -1;
+  return (cin == 4 || cin == 8) ? 9 * cin * kCout : cin == 64 ? 9 * 64 * kCout + 2 * kWinoHalf + kW2UFloats : -1;
 }
 
 int bk_conv3x3_form(int N, int cin) { return cin == 64 && N % 2 == 0 && !direct_only() ? 1 : 0; }
@@ -555,6 +809,36 @@ int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, cons
                       "hipFuncSetAttribute") != BK_OK)
           return BK_EHIP;
       attr_set = true;
+    }
+    if (bk_conv3x3_form(N, cin) == 1 && !wino_form1()) {
+      static bool w2attr = false;
+      const int lds = (int)(sizeof(float) * 2 * kW2VBuf);
+      if (!w2attr) {
+        const void* fns[4] = {(const void*)k_conv3x3_wino2<true, true>, (const void*)k_conv3x3_wino2<true, false>,
+                              (const void*)k_conv3x3_wino2<false, true>, (const void*)k_conv3x3_wino2<false, false>};
+        for (const void* fn : fns)
+          if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                        "hipFuncSetAttribute") != BK_OK)
+            return BK_EHIP;
+        w2attr = true;
+      }
+      BK_REQUIRE(total * 64 < (1ll << 31), "bk_conv3x3: batch too large");
+      const float* u2 = wpacked + 9 * 64 * kCout + 2 * kWinoHalf;
+      const int tiles = (int)(total / 4);
+      const int g = blocks >= 8 ? blocks / 8 * 8 : 8;
+      if (relu && residual)
+        hipLaunchKernelGGL((k_conv3x3_wino2<true, true>), dim3(g), dim3(kW2Threads), lds, s, x, u2, bias, residual, y, N,
+                           tiles);
+      else if (relu)
+        hipLaunchKernelGGL((k_conv3x3_wino2<true, false>), dim3(g), dim3(kW2Threads), lds, s, x, u2, bias, residual, y, N,
+                           tiles);
+      else if (residual)
+        hipLaunchKernelGGL((k_conv3x3_wino2<false, true>), dim3(g), dim3(kW2Threads), lds, s, x, u2, bias, residual, y,
+                           N, tiles);
+      else
+        hipLaunchKernelGGL((k_conv3x3_wino2<false, false>), dim3(g), dim3(kW2Threads), lds, s, x, u2, bias, residual, y,
+                           N, tiles);
+      return launch_check("k_conv3x3_wino2");
     }
     if (bk_conv3x3_form(N, cin) == 1) {
       static bool wattr = false;

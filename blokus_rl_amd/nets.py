@@ -199,9 +199,10 @@ _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 
 
 def pack_winograd(w: torch.Tensor) -> torch.Tensor:
-    """[64, 64, 3, 3] -> the Winograd F(2x2,3x3) form's U = G w G^T (computed in fp64, stored f32) in
-    k_conv3x3_wino's LDS order: flat [2 halves h][2 blocks k][16 positions p][16 k-steps s][64 lanes],
-    element = U[32h + 16k + (l & 15), 16 * (l >> 4) + s, p // 4, p % 4]."""
+    """[64, 64, 3, 3] -> the Winograd F(2x2,3x3) form's U = G w G^T (computed in fp64, stored f32),
+    twice: in k_conv3x3_wino's LDS order (form 1): flat [2 halves h][2 blocks k][16 positions p]
+    [16 k-steps s][64 lanes], element = U[32h + 16k + (l & 15), 16 * (l >> 4) + s, p // 4, p % 4];
+    then in k_conv3x3_wino2's register order (form 2, below)."""
     assert w.shape == (64, 64, 3, 3)
     G = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
     U = torch.einsum("ik,ockl,jl->ocij", G, w.double(), G).reshape(64, 64, 16)  # [cout][cin][p]
@@ -212,7 +213,15 @@ def pack_winograd(w: torch.Tensor) -> torch.Tensor:
     st = torch.arange(16, device=dev).view(1, 1, 1, 16, 1)
     lane = torch.arange(64, device=dev).view(1, 1, 1, 1, 64)
     out = U[32 * h + 16 * k + (lane & 15), 16 * (lane >> 4) + st, pos]
-    return out.float().contiguous().view(-1)
+    # form 2 (k_conv3x3_wino2, U in registers): [4 blocks kb][64 q][64 lanes][4 e], i = 4q + e,
+    # element = U[16kb + (l & 15), 4 * (i // 16) + (l >> 4), i % 16]
+    kb = torch.arange(4, device=dev).view(4, 1, 1, 1)
+    q = torch.arange(64, device=dev).view(1, 64, 1, 1)
+    l2 = torch.arange(64, device=dev).view(1, 1, 64, 1)
+    e = torch.arange(4, device=dev).view(1, 1, 1, 4)
+    i = 4 * q + e
+    out2 = U[16 * kb + (l2 & 15), 4 * (i // 16) + (l2 >> 4), i % 16]
+    return torch.cat([out.float().contiguous().view(-1), out2.float().contiguous().view(-1)])
 
 
 def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bool,

@@ -41,10 +41,20 @@ def test_conv3x3_matches_torch(B, N, cin, relu, use_res):
     assert bool((err <= 1e-5 * bound).all()), float((err / bound).max())
 
 
+@pytest.mark.parametrize("B,N,cin", [(256, 20, 64), (3, 20, 64), (33, 20, 64), (300, 20, 64), (9, 8, 64),
+                                     (3, 2, 64), (2, 14, 64)])
+@pytest.mark.parametrize("relu,use_res", [(True, False), (True, True), (False, True)])
+def test_conv3x3_winograd_form1_matches_torch(B, N, cin, relu, use_res, monkeypatch):
+    """BK_CONV_WINO=1: the Winograd form with U in LDS (k_conv3x3_wino) instead of form 2."""
+    monkeypatch.setenv("BK_CONV_WINO", "1")
+    test_conv3x3_matches_torch(B, N, cin, relu, use_res)
+
+
 @pytest.mark.parametrize("B", [1, 37, 256])
 def test_winograd_and_direct_forms_agree(B, monkeypatch):
-    """Even N runs the Winograd F(2x2,3x3) form, BK_CONV_DIRECT=1 the direct one: both f32,
-    both within the f32 bound of the fp64 convolution, and close to each other."""
+    """Even N runs the Winograd F(2x2,3x3) form (2, or 1 with BK_CONV_WINO=1), BK_CONV_DIRECT=1
+    the direct one: all f32, all within the f32 bound of the fp64 convolution, and close to each
+    other (the two Winograd forms group the channel sum differently, so they agree to rounding)."""
     from blokus_rl_amd.nets import conv3x3, pack_conv3x3
 
     g = torch.Generator(device="cuda").manual_seed(B)
@@ -54,11 +64,14 @@ def test_winograd_and_direct_forms_agree(B, monkeypatch):
     wp = pack_conv3x3(w)
     xin = x.contiguous(memory_format=torch.channels_last)
     y_w = conv3x3(xin, wp, b, True)
+    monkeypatch.setenv("BK_CONV_WINO", "1")
+    y_w1 = conv3x3(xin, wp, b, True)
     monkeypatch.setenv("BK_CONV_DIRECT", "1")
     y_d = conv3x3(xin, wp, b, True)
     torch.cuda.synchronize()
     ref, bound = _ref(x, w, b, True, None)
-    for y in (y_w, y_d):
+    assert bool(((y_w.double() - y_w1.double()).abs() <= 2e-5 * bound).all())
+    for y in (y_w, y_w1, y_d):
         assert bool(((y.double() - ref).abs() <= 1e-5 * bound).all())
     assert bool(((y_w.double() - y_d.double()).abs() <= 2e-5 * bound).all())
     assert not torch.equal(y_w, y_d)  # two different kernels really ran
