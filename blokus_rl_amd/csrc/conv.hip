@@ -635,8 +635,10 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __
       ur[q] = usrc[q * kWave];
       __builtin_amdgcn_sched_barrier(0);  // keep k-step order: the peeled group waits step by step
     }
+    transform_part(raw0, 0, 0);
+    W2STAMP(27, __builtin_amdgcn_s_memtime());
 #pragma unroll
-    for (int k = 0; k < 8; ++k) transform_part(raw0, 0, k);
+    for (int k = 1; k < 8; ++k) transform_part(raw0, 0, k);
   }
   W2STAMP(28, __builtin_amdgcn_s_memtime());
   __syncthreads();
@@ -676,7 +678,14 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __
         for (int p = 0; p < 16; ++p) vb[(s + 1) & 1][p] = vsrc[((s + 1) * 16 + p) * 64];
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (s >= 8) transform_part(raw, buf ^ 1, s - 8);
+#ifndef BK_W2_TF_FROM
+#define BK_W2_TF_FROM 8
+#endif
+      if (s >= BK_W2_TF_FROM) {
+        constexpr int per = 8 / (16 - BK_W2_TF_FROM);
+#pragma unroll
+        for (int k = 0; k < per; ++k) transform_part(raw, buf ^ 1, per * (s - BK_W2_TF_FROM) + k);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int p = 0; p < 16; ++p) {

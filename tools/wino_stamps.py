@@ -69,4 +69,10 @@ if form2:
     out["g2_steps_12_15"] = q(g2[:, 9] - g2[:, 25])
     g0 = st[:, :nw][live]
     out["g0_loop"] = q(g0[:, 3] - g0[:, 2])
+    out["prologue_first_window"] = q(g0[:, 27] - g0[:, 0])
+    out["prologue_transform"] = q(g0[:, 28] - g0[:, 27])
+    out["prologue_barrier"] = q(g0[:, 1] - g0[:, 28])
+    blk = st[:, :nw, 0]
+    ok = (blk > 0).all(axis=1)
+    out["block_start_skew"] = q(blk[ok].max(axis=1) - blk[ok].min(axis=1))
 print(json.dumps(out, indent=1))
