@@ -79,14 +79,15 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
 
 
 def time_leaf_conv(sp, reps: int = 5):
-    """The dominant kernel of the self-play step, k_conv3x3 (the 64 -> 64 residual-block convs of
-    the leaf evaluator at the leaf batch), timed live with HIP events on the stream it is
-    launched on: `reps` eager forwards of the leaf net on the search's last leaf batch, one event
-    pair around each residual-block conv launch (the graph-captured forward is the same kernel
-    sequence). -> (mean ms per launch, FLOP per launch, form, direct-conv FLOP per launch) or None
-    (no HIP ResNet). FLOP = the arithmetic the kernel's MFMAs execute: for the Winograd
-    F(2x2,3x3) form 2*16*64*64 per 2x2 output tile (16 transform-domain GEMMs), for the direct
-    form 2*9*64*64 per output pixel."""
+    """The dominant kernel of the self-play step, timed live with HIP events on the stream it is
+    launched on: `reps` eager forwards of the leaf net on the search's last leaf batch (the
+    graph-captured forward is the same kernel sequence), one event pair around each launch of
+    k_tower_wino (the fused residual tower, bk_resnet_tower) or, when the tower runs per layer
+    (BK_TOWER=0 or an unsupported board size), around each residual-block k_conv3x3 launch.
+    -> dict(ms per launch, FLOP per launch, kernel name, direct-conv FLOP per launch, launches per
+    leaf batch) or None (no HIP ResNet). FLOP = the arithmetic the kernel's MFMAs execute: for the
+    Winograd F(2x2,3x3) form 2*16*64*64 per 2x2 output tile and conv (16 transform-domain GEMMs),
+    for the direct form 2*9*64*64 per output pixel and conv."""
     from .. import nets
     from ..engine import load_library
     from ..nets import LeafResNet
@@ -95,35 +96,47 @@ def time_leaf_conv(sp, reps: int = 5):
     if not isinstance(model, LeafResNet) or not model.native or not len(model.f.blocks):
         return None
     G, N = sp.G, sp.eng.N
+    nconv = 2 * len(model.f.blocks)
     obs = sp.evaluator.static_obs
     st = torch.cuda.current_stream(sp.eng.device)
     events = []
-    orig = nets.conv3x3
+    orig_conv, orig_tower = nets.conv3x3, nets.resnet_tower
 
-    def timed(x, w, b, relu, residual=None):
-        if x.shape[1] != 64:  # the stem (planar observation input) is not a residual-block conv
-            return orig(x, w, b, relu, residual)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        y = orig(x, w, b, relu, residual)
-        e1.record(st)
-        events.append((e0, e1))
-        return y
+    def timed(fn):
+        def run(*a, **k):
+            if fn is orig_conv and a[0].shape[1] != 64:  # the stem (planar observation input)
+                return fn(*a, **k)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            y = fn(*a, **k)
+            e1.record(st)
+            events.append((e0, e1, fn is orig_tower))
+            return y
+        return run
 
-    nets.conv3x3 = timed
+    nets.conv3x3, nets.resnet_tower = timed(orig_conv), timed(orig_tower)
     try:
         model(obs)  # warm
         events.clear()
         for _ in range(reps):
             model(obs)
     finally:
-        nets.conv3x3 = orig
+        nets.conv3x3, nets.resnet_tower = orig_conv, orig_tower
     torch.cuda.synchronize()
-    ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
-    direct = 2.0 * G * N * N * 64 * 9 * 64
+    if not events:
+        return None
+    fused = events[0][2]
+    ms = sum(a.elapsed_time(b) for a, b, _ in events) / len(events)
+    layers = nconv if fused else 1
+    direct = 2.0 * G * N * N * 64 * 9 * 64 * layers
     if load_library().bk_conv3x3_form(N, 64) == 1:
-        return ms, 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2, "winograd", direct
-    return ms, direct, "direct", direct
+        flop = 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2 * layers
+        name = ("k_tower_wino (the fused residual tower: %d Winograd F(2x2,3x3) f32 MFMA convs 64->64, "
+                "bias/ReLU/residual fused, one workgroup per board)" % nconv if fused else
+                "k_conv3x3_wino2 (Winograd F(2x2,3x3), f32 MFMA, 64->64, fused bias+ReLU)")
+    else:
+        flop, name = direct, "k_conv3x3 (direct, f32 MFMA, 64->64, fused bias+ReLU)"
+    return {"ms": ms, "flop": flop, "kernel": name, "direct": direct, "launches": 1 if fused else nconv}
 
 
 def bench_selfplay(args, world, rank):
@@ -166,7 +179,9 @@ def bench_selfplay(args, world, rank):
                             "frac": achieved / HBM_PEAK, "traffic": None,
                             "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms},
         "net_roofline": {"bound": "mfma",
-                         "kernel": "leaf ResNet forward (k_conv3x3 x 11, k_resnet_heads, hipBLASLt policy Linear)",
+                         "kernel": "leaf ResNet forward (stem k_conv3x3, k_tower_wino, k_resnet_heads, sparse policy "
+                                   "head); FLOP counted as the direct-convolution network (347.5 MFLOP/leaf), so "
+                                   "frac can exceed 1 with the Winograd tower",
                          "achieved": net_flops / (ms.get("net", 1e9) * 1e-3) / 1e12 if ms else None,
                          "peak": net_peak / 1e12, "unit": "TFLOP/s",
                          "frac": (net_flops / (ms["net"] * 1e-3)) / net_peak if ms else None},
@@ -174,15 +189,14 @@ def bench_selfplay(args, world, rank):
         "engine_counters": delta,
     }
     if conv is not None:
-        cms, cflop, form, dflop = conv
-        kname = ("k_conv3x3_wino (Winograd F(2x2,3x3), f32 MFMA" if form == "winograd"
-                 else "k_conv3x3 (direct, f32 MFMA") + ", 64->64, fused bias+ReLU)"
-        out["roofline"] = {"bound": "mfma", "kernel": kname,
+        cms, cflop, dflop = conv["ms"], conv["flop"], conv["direct"]
+        out["roofline"] = {"bound": "mfma", "kernel": conv["kernel"],
                            "achieved": cflop / (cms * 1e-3) / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
                            "frac": cflop / (cms * 1e-3) / FP32_PEAK, "traffic": None, "kernel_ms": cms,
                            "flop_per_launch": cflop, "units_per_launch": G,
                            "direct_conv_equiv_tflops": dflop / (cms * 1e-3) / 1e12,
-                           "launches_per_sim_step": 10, "share_of_sim_step": 10 * cms / (elapsed / steps_sim * 1e3)}
+                           "launches_per_sim_step": conv["launches"],
+                           "share_of_sim_step": conv["launches"] * cms / (elapsed / steps_sim * 1e3)}
     else:
         out["roofline"] = out["search_roofline"]
     return out

@@ -540,59 +540,37 @@ __device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {
 constexpr int kW2Threads = 256;
 constexpr int kW2UFloats = 4 * 64 * kWave * 4;  // [4 kb][64 q][64 lanes][4]: (s, p) = divmod(4q + e, 16)
 constexpr int kW2VBuf = 16 * 16 * 16 * 4;      // floats per V buffer: [16 s][16 p][16 t][4 g]
+constexpr unsigned kW2Out = 0x7fff0000u;       // a window offset beyond any buffer: the load returns 0
 
-template <bool RELU, bool RES>
-__global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __restrict__ x,
-                                                                 const float* __restrict__ u2,
-                                                                 const float* __restrict__ bias,
-                                                                 const float* __restrict__ res,
-                                                                 float* __restrict__ y, int N, int tiles) {
-  extern __shared__ __attribute__((aligned(16))) float v_lds[];  // [2 buf][16 s][16 p][16 t][4 g]
-  const int xcd = blockIdx.x & 7, cu = blockIdx.x >> 3, ncu = gridDim.x >> 3;
-  const int groups = (tiles + 15) >> 4;
-  const int g_begin = (int)((int64_t)groups * xcd / 8), g_end = (int)((int64_t)groups * (xcd + 1) / 8);
-  const int range = g_end - g_begin;
-  const int c_lo = g_begin + (int)((int64_t)range * cu / ncu), c_hi = g_begin + (int)((int64_t)range * (cu + 1) / ncu);
-  if (c_lo == c_hi) return;
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  W2STAMP(0, __builtin_amdgcn_s_memtime());
-  W2STAMP(30, __builtin_amdgcn_s_memrealtime());
-  const int T2 = N >> 1, tpb = T2 * T2;
-  // transform role: tile tt of the group, k-step (channel quad) sq
-  const int tt = l & 15, sq = (wave << 2) | (l >> 4);
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, tiles * 1024, 0x00020000);
-  constexpr unsigned kOut = 0x7fff0000u;
-  // window offsets, branch-free: a row or column off the board (or a tile past the end) gets a
-  // base of kOut, so the sum lands beyond the buffer and the load returns 0. Also returns the
-  // group's output pixel index for lane l's tile (the epilogue's, -1 past the end).
-  auto window = [&](int grp, unsigned (&off)[16]) {
-    const unsigned tile = (unsigned)(grp * 16 + tt);
-    const bool tv = tile < (unsigned)tiles;
-    const unsigned b = tile / (unsigned)tpb, r = tile - b * (unsigned)tpb;
-    const int ty = (int)(r / (unsigned)T2), tx = (int)r - ty * T2;
-    const int rbase = ((int)b * N + 2 * ty - 1) * N * 256 + 16 * sq, cbase = (2 * tx - 1) * 256;
+// Per-lane context of the form-2 kernels: the input buffer, the LDS V buffers, the lane's
+// transform role (tile tt of the group, channel quad sq) and MFMA role (wave = output block).
+struct W2Lane {
+  float* v_lds;
+  __amdgpu_buffer_rsrc_t xr;
+  int wave, l, tt, sq;
+  __device__ f32x4 ld(unsigned o) const {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
+  }
+  // window offsets of the lane's tile at tile coordinates (ty, tx) of the board whose row 0 is at
+  // byte rowbase0, branch-free: a row or column off the board (or an invalid tile) gets a base of
+  // kW2Out, so the sum lands beyond the buffer and the load returns 0
+  __device__ void window(bool tv, int N, int rowbase0, int ty, int tx, unsigned (&off)[16]) const {
+    const int rbase = rowbase0 + (2 * ty - 1) * N * 256 + 16 * sq, cbase = (2 * tx - 1) * 256;
     unsigned rb[4], cb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int yy = 2 * ty - 1 + i, xx = 2 * tx - 1 + i;
-      rb[i] = tv && yy >= 0 && yy < N ? (unsigned)(rbase + i * N * 256) : kOut;
-      cb[i] = xx >= 0 && xx < N ? (unsigned)(cbase + i * 256) : kOut;
+      rb[i] = tv && yy >= 0 && yy < N ? (unsigned)(rbase + i * N * 256) : kW2Out;
+      cb[i] = xx >= 0 && xx < N ? (unsigned)(cbase + i * 256) : kW2Out;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) off[4 * i + j] = rb[i] + cb[j];
-  };
-  auto out_pixel = [&](int grp) {  // top-left output pixel of lane l's tile in group grp
-    const unsigned tile = (unsigned)(grp * 16 + (l & 15));
-    const unsigned b = tile / (unsigned)tpb, r = tile - b * (unsigned)tpb;
-    const int ty = (int)(r / (unsigned)T2), tx = (int)r - ty * T2;
-    return tile < (unsigned)tiles ? ((int)b * N + 2 * ty) * N + 2 * tx : -1;
-  };
-  auto ld = [&](unsigned o) { return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0)); };
-  // B^T d B of this thread's 4 channels as two packed pairs h -> V[buf][sq][p][tt][2h, 2h+1], in 8
+  }
+  // B^T d B of the lane's 4 channels as two packed pairs h -> V[buf][sq][p][tt][2h, 2h+1], in 8
   // parts k = (h, i): row i of the 4x4 result, t_i = (B^T d)_i from two window rows, v_i = t_i B
-  auto transform_part = [&](const f32x4 (&raw)[16], int buf, int k) {
+  __device__ void transform_part(const f32x4 (&raw)[16], int buf, int k) const {
     const int h = k >> 2, i = k & 3;
     float* dst = v_lds + buf * kW2VBuf + sq * 1024 + tt * 4 + 2 * h;
     auto d = [&](int q) { return h ? raw[q].zw : raw[q].xy; };
@@ -608,148 +586,265 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __
     *reinterpret_cast<f32x2*>(dst + (4 * i + 1) * 64) = pk_add(t[1], t[2]);
     *reinterpret_cast<f32x2*>(dst + (4 * i + 2) * 64) = pk_sub(t[2], t[1]);
     *reinterpret_cast<f32x2*>(dst + (4 * i + 3) * 64) = pk_sub(t[1], t[3]);
-  };
-  // prologue: the first two groups' windows and the bias, then this wave's U (AGPRs) for k-steps
-  // 0 and 1, ur[4s + p/4][p%4] = U[16 wave + (l & 15)][4s + (l >> 4)][p]. The first group's MFMA
-  // loop (a peeled copy of the group body, whose window loads are these) loads U two k-steps
-  // ahead and waits for each k-step's U as it arrives: U streams in under its MFMAs.
-  f32x4 ur[64];
-  f32x4 raw[16];
+  }
+  // A^T M A + residual + ReLU of the lane's tile (top-left output pixel opix, -1 = none) for
+  // channels 16 wave + 4 (l >> 4) + 0..3, on packed channel pairs; y / res point at pixel 0 of
+  // their [..][N][N][64] buffers
+  __device__ void epilogue(const f32x4 (&acc)[16], int opix, int N, bool relu, const float* res, float* y) const {
+    if (opix < 0) return;
+    f32x2 yv[4][2];  // [pixel 2i + j][pair h]
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      auto m = [&](int q) { return h ? acc[q].zw : acc[q].xy; };
+      f32x2 u2v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        u2v[j] = pk_add(pk_add(m(j), m(4 + j)), m(8 + j));
+        u2v[4 + j] = pk_sub(pk_sub(m(4 + j), m(8 + j)), m(12 + j));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        yv[2 * i][h] = pk_add(pk_add(u2v[4 * i + 0], u2v[4 * i + 1]), u2v[4 * i + 2]);
+        yv[2 * i + 1][h] = pk_sub(pk_sub(u2v[4 * i + 1], u2v[4 * i + 2]), u2v[4 * i + 3]);
+      }
+    }
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const size_t o = (size_t)(opix + (px >> 1) * N + (px & 1)) * 64 + 16 * wave + 4 * (l >> 4);
+      f32x2 lo = yv[px][0], hi = yv[px][1];
+      if (res) {
+        const f32x4 rr = *reinterpret_cast<const f32x4*>(res + o);
+        lo = pk_add(lo, rr.xy);
+        hi = pk_add(hi, rr.zw);
+      }
+      f32x4 out = f32x4{lo.x, lo.y, hi.x, hi.y};
+      if (relu) {
+        out.x = fmaxf(out.x, 0.0f);
+        out.y = fmaxf(out.y, 0.0f);
+        out.z = fmaxf(out.z, 0.0f);
+        out.w = fmaxf(out.w, 0.0f);
+      }
+      *reinterpret_cast<f32x4*>(y + o) = out;
+    }
+  }
+};
+
+// The first group's U: this wave's k-steps 0 and 1 (the rest stream in under the first group's
+// MFMAs, w2_group<true>), in k-step order, ur[4s + p/4][p%4] = U[16 wave + (l & 15)][4s + (l >> 4)][p]
+__device__ __forceinline__ void w2_load_u01(f32x4 (&ur)[64], const f32x4* usrc) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    ur[q] = usrc[q * kWave];
+    __builtin_amdgcn_sched_barrier(0);  // keep k-step order: the first group waits step by step
+  }
+}
+
+// One group of 16 tiles, V already in LDS buffer buf: 16 k-steps of 16 MFMAs (A = U from AGPRs
+// via inline asm, B = V from LDS one step ahead, accumulators in VGPRs, the bias as the initial
+// accumulator of position (1,1)); meanwhile the next group's window loads go out over steps 0-3
+// (offsets from next_window() at step 0; FIRST: already in raw) and its transform runs in 8 parts
+// over steps 8-15 into V[buf ^ 1]; FIRST also loads U two k-steps ahead. f32 MFMAs run on the
+// SIMD's vector ALUs, so a VALU instruction beside them is not hidden and every MFMA <-> VALU
+// switch costs ~10 cycles (tools/probe/mfma_fill.hip): the MFMA stream carries no VALU, and the
+// VALU work comes in batches. Returns with acc ready for the epilogue.
+template <bool FIRST, class NextWindow>
+__device__ __forceinline__ void w2_group(const W2Lane& c, f32x4 (&ur)[64], f32x4 (&raw)[16], const f32x4* usrc,
+                                         f32x4 bias4, int buf, NextWindow next_window, f32x4 (&acc)[16]) {
+  const float* vsrc = c.v_lds + buf * kW2VBuf + (c.l & 15) * 4 + (c.l >> 4);  // V[buf][s][p][t][g]
+  float vb[2][16];
   unsigned off[16];
-  f32x4 bias4;
-  const f32x4* usrc = reinterpret_cast<const f32x4*>(u2) + (size_t)wave * 64 * kWave + l;
-  {
-    f32x4 raw0[16];
-    window(c_lo, off);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) raw0[q] = ld(off[q]);
-    window(c_lo + 1 < c_hi ? c_lo + 1 : c_lo, off);
+  for (int p = 0; p < 16; ++p) vb[0][p] = vsrc[p * 64];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) raw[q] = ld(off[q]);
-    // the bias as the initial accumulator of position (1,1) (p = 5): the output transform adds
-    // M(1,1) to all four pixels of a tile
-    bias4 = *reinterpret_cast<const f32x4*>(bias + 16 * wave + 4 * (l >> 4));
+  for (int s = 0; s < 16; ++s) {
+    if (s == 0 && !FIRST) next_window(off);
+    if (s < 4 && !FIRST) {
+#pragma unroll
+      for (int q = 4 * s; q < 4 * s + 4; ++q) raw[q] = c.ld(off[q]);
+    }
+    if (FIRST && s + 2 < 16) {  // U of k-step s + 2, in order
+#pragma unroll
+      for (int q = 4 * (s + 2); q < 4 * (s + 2) + 4; ++q) {
+        ur[q] = usrc[q * kWave];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (s + 1 < 16) {  // B operands of the next k-step, before any VALU work of this one
+#pragma unroll
+      for (int p = 0; p < 16; ++p) vb[(s + 1) & 1][p] = vsrc[((s + 1) * 16 + p) * 64];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (s >= 8) c.transform_part(raw, buf ^ 1, s - 8);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {  // k-steps 0 and 1; the peeled group loads the rest
-      ur[q] = usrc[q * kWave];
-      __builtin_amdgcn_sched_barrier(0);  // keep k-step order: the peeled group waits step by step
+    for (int p = 0; p < 16; ++p) {
+      const float ua = ur[4 * s + (p >> 2)][p & 3];
+      const float vv = vb[s & 1][p];
+      if (s == 0 && p == 5)
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %3" : "=&v"(acc[p]) : "a"(ua), "v"(vv), "v"(bias4));
+      else if (s == 0)
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(acc[p]) : "a"(ua), "v"(vv));
+      else
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc[p]) : "a"(ua), "v"(vv));
     }
-    transform_part(raw0, 0, 0);
-    W2STAMP(27, __builtin_amdgcn_s_memtime());
-#pragma unroll
-    for (int k = 1; k < 8; ++k) transform_part(raw0, 0, k);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  W2STAMP(28, __builtin_amdgcn_s_memtime());
+  // the accumulators are written by MFMAs the compiler cannot see: wait out the XDL write ->
+  // VALU read latency before the epilogue reads them
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+
+// One conv layer over B*N*N/4 tiles (any batch): 16-tile groups, the 8 XCDs take contiguous
+// eighths of them, each CU a contiguous run (its windows share board rows in L1/L2).
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __restrict__ x,
+                                                                 const float* __restrict__ u2,
+                                                                 const float* __restrict__ bias,
+                                                                 const float* __restrict__ res,
+                                                                 float* __restrict__ y, int N, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) float v_lds[];  // [2 buf][16 s][16 p][16 t][4 g]
+  const int xcd = blockIdx.x & 7, cu = blockIdx.x >> 3, ncu = gridDim.x >> 3;
+  const int groups = (tiles + 15) >> 4;
+  const int g_begin = (int)((int64_t)groups * xcd / 8), g_end = (int)((int64_t)groups * (xcd + 1) / 8);
+  const int range = g_end - g_begin;
+  const int c_lo = g_begin + (int)((int64_t)range * cu / ncu), c_hi = g_begin + (int)((int64_t)range * (cu + 1) / ncu);
+  if (c_lo == c_hi) return;
+  W2Lane c;
+  c.v_lds = v_lds;
+  c.wave = threadIdx.x >> 6;
+  c.l = threadIdx.x & 63;
+  c.tt = c.l & 15;
+  c.sq = (c.wave << 2) | (c.l >> 4);
+  c.xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, tiles * 1024, 0x00020000);
+  const int l = c.l, wave = c.wave;
+  W2STAMP(0, __builtin_amdgcn_s_memtime());
+  W2STAMP(30, __builtin_amdgcn_s_memrealtime());
+  const int T2 = N >> 1, tpb = T2 * T2;
+  auto window = [&](int grp, unsigned (&off)[16]) {
+    const unsigned tile = (unsigned)(grp * 16 + c.tt);
+    const unsigned b = tile / (unsigned)tpb, r = tile - b * (unsigned)tpb;
+    const int ty = (int)(r / (unsigned)T2);
+    c.window(tile < (unsigned)tiles, N, (int)b * N * N * 256, ty, (int)r - ty * T2, off);
+  };
+  auto out_pixel = [&](int grp) {  // top-left output pixel of lane l's tile in group grp
+    const unsigned tile = (unsigned)(grp * 16 + (l & 15));
+    const unsigned b = tile / (unsigned)tpb, r = tile - b * (unsigned)tpb;
+    const int ty = (int)(r / (unsigned)T2), tx = (int)r - ty * T2;
+    return tile < (unsigned)tiles ? ((int)b * N + 2 * ty) * N + 2 * tx : -1;
+  };
+  // prologue: the first two groups' windows and the bias, then U of k-steps 0 and 1; the first
+  // group's MFMA loop streams in the rest of U
+  const f32x4* usrc = reinterpret_cast<const f32x4*>(u2) + (size_t)wave * 64 * kWave + l;
+  f32x4 ur[64];
+  f32x4 raw[16];
+  f32x4 bias4;
+  {
+    f32x4 raw0[16];
+    unsigned off[16];
+    window(c_lo, off);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) raw0[q] = c.ld(off[q]);
+    window(c_lo + 1 < c_hi ? c_lo + 1 : c_lo, off);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) raw[q] = c.ld(off[q]);
+    bias4 = *reinterpret_cast<const f32x4*>(bias + 16 * wave + 4 * (l >> 4));
+    __builtin_amdgcn_sched_barrier(0);
+    w2_load_u01(ur, usrc);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c.transform_part(raw0, 0, k);
+  }
   __syncthreads();
   W2STAMP(1, __builtin_amdgcn_s_memtime());
-  const float* vrd = v_lds + (l & 15) * 4 + (l >> 4);  // lane (g, t) reads V[.][s][p][t][g]
-  int opix = out_pixel(c_lo);
-  // one group: 16 k-steps of 16 MFMAs (A = U from AGPRs, B = V from LDS one step ahead); the next
-  // group's window loads go out over steps 0-3 (offsets at step 0) and its transform runs in 8
-  // parts over steps 8-15; then the output transform and one barrier. The last group re-reads
-  // its own window into the idle V buffer, so loads and transforms stay unconditional.
-  auto run_group = [&](int grp, int buf, auto first) {
+  // the last group re-reads its own window into the idle V buffer, so loads and transforms stay
+  // unconditional (no load pending across the loop's back edge)
+  auto group = [&](int grp, int buf, auto first) {
     W2STAMP(2 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
     const int nxt = grp + 1 < c_hi ? grp + 1 : grp;
     f32x4 acc[16];
-    const float* vsrc = vrd + buf * kW2VBuf;
-    float vb[2][16];
-#pragma unroll
-    for (int p = 0; p < 16; ++p) vb[0][p] = vsrc[p * 64];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      if (s == 0 && !decltype(first)::value) window(nxt, off);
-      if (s < 4 && !decltype(first)::value) {
-#pragma unroll
-        for (int q = 4 * s; q < 4 * s + 4; ++q) raw[q] = ld(off[q]);
-      }
-      if (decltype(first)::value && s + 2 < 16) {  // U of k-step s + 2, in order
-#pragma unroll
-        for (int q = 4 * (s + 2); q < 4 * (s + 2) + 4; ++q) {
-          ur[q] = usrc[q * kWave];
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (!decltype(first)::value && grp - c_lo == 2 && (s == 4 || s == 8 || s == 12))
-        W2STAMP(22 + s / 4, __builtin_amdgcn_s_memtime());
-      if (s + 1 < 16) {  // B operands of the next k-step, before any VALU work of this one
-#pragma unroll
-        for (int p = 0; p < 16; ++p) vb[(s + 1) & 1][p] = vsrc[((s + 1) * 16 + p) * 64];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#ifndef BK_W2_TF_FROM
-#define BK_W2_TF_FROM 8
-#endif
-      if (s >= BK_W2_TF_FROM) {
-        constexpr int per = 8 / (16 - BK_W2_TF_FROM);
-#pragma unroll
-        for (int k = 0; k < per; ++k) transform_part(raw, buf ^ 1, per * (s - BK_W2_TF_FROM) + k);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int p = 0; p < 16; ++p) {
-        const float ua = ur[4 * s + (p >> 2)][p & 3];
-        const float vv = vb[s & 1][p];
-        if (s == 0 && p == 5)
-          asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %3" : "=&v"(acc[p]) : "a"(ua), "v"(vv), "v"(bias4));
-        else if (s == 0)
-          asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(acc[p]) : "a"(ua), "v"(vv));
-        else
-          asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc[p]) : "a"(ua), "v"(vv));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // the accumulators are written by MFMAs the compiler cannot see: wait out the XDL
-    // write -> VALU read latency before the epilogue reads them
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    w2_group<decltype(first)::value>(c, ur, raw, usrc, bias4, buf, [&](unsigned (&off)[16]) { window(nxt, off); },
+                                     acc);
     W2STAMP(3 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
-    // A^T M A for (lane l's tile; channels 16 wave + 4 (l >> 4) + 0..3) on packed channel pairs
-    if (opix >= 0) {
-      f32x2 yv[4][2];  // [pixel 2i + j][pair h]
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        auto m = [&](int q) { return h ? acc[q].zw : acc[q].xy; };
-        f32x2 u2v[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          u2v[j] = pk_add(pk_add(m(j), m(4 + j)), m(8 + j));
-          u2v[4 + j] = pk_sub(pk_sub(m(4 + j), m(8 + j)), m(12 + j));
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          yv[2 * i][h] = pk_add(pk_add(u2v[4 * i + 0], u2v[4 * i + 1]), u2v[4 * i + 2]);
-          yv[2 * i + 1][h] = pk_sub(pk_sub(u2v[4 * i + 1], u2v[4 * i + 2]), u2v[4 * i + 3]);
-        }
-      }
-#pragma unroll
-      for (int px = 0; px < 4; ++px) {
-        const size_t o = (size_t)(opix + (px >> 1) * N + (px & 1)) * 64 + 16 * wave + 4 * (l >> 4);
-        f32x2 lo = yv[px][0], hi = yv[px][1];
-        if (RES) {
-          const f32x4 rr = *reinterpret_cast<const f32x4*>(res + o);
-          lo = pk_add(lo, rr.xy);
-          hi = pk_add(hi, rr.zw);
-        }
-        f32x4 out = f32x4{lo.x, lo.y, hi.x, hi.y};
-        if (RELU) {
-          out.x = fmaxf(out.x, 0.0f);
-          out.y = fmaxf(out.y, 0.0f);
-          out.z = fmaxf(out.z, 0.0f);
-          out.w = fmaxf(out.w, 0.0f);
-        }
-        *reinterpret_cast<f32x4*>(y + o) = out;
-      }
-    }
-    opix = out_pixel(nxt);
+    c.epilogue(acc, out_pixel(grp), N, RELU, RES ? res : nullptr, y);
     __syncthreads();  // V[buf ^ 1] complete for the next group; V[buf] free to be overwritten
     W2STAMP(4 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
   };
-  run_group(c_lo, 0, std::true_type{});  // peeled: its MFMAs wait for U k-step by k-step
+  group(c_lo, 0, std::true_type{});
   int buf = 1;
-  for (int grp = c_lo + 1; grp < c_hi; ++grp, buf ^= 1) run_group(grp, buf, std::false_type{});
+  for (int grp = c_lo + 1; grp < c_hi; ++grp, buf ^= 1) group(grp, buf, std::false_type{});
   W2STAMP(29, __builtin_amdgcn_s_memtime());
   W2STAMP(31, __builtin_amdgcn_s_memrealtime());
+}
+
+// The inference ResNet's whole residual tower (models/blokus_nnet.py:140-141, BN folded) in one
+// launch, one workgroup per board: layer l = conv3x3 (Winograd form 2) over the board, ReLU on
+// even layers (each block's first conv), the last layer adds the tower input and takes the ReLU;
+// intermediate activations ping-pong between hA and hB. A board's tiles depend only on the same
+// board, so layers are separated by a workgroup barrier instead of a kernel boundary: no launch
+// gap, no cold L2 after a cross-XCD release, and the next layer's first windows are L2-hot.
+template <int N>
+__global__ __launch_bounds__(kW2Threads, 1) void k_tower_wino(const float* __restrict__ x0, float* hA, float* hB,
+                                                              float* __restrict__ out,
+                                                              const float* __restrict__ u2all,
+                                                              const float* __restrict__ biasall, int nlayers) {
+  extern __shared__ __attribute__((aligned(16))) float v_lds[];  // [2 buf][16 s][16 p][16 t][4 g]
+  constexpr int T2 = N / 2, TPB = T2 * T2, NG = (TPB + 15) / 16;
+  const size_t board = (size_t)blockIdx.x * N * N * 64;
+  W2Lane c;
+  c.v_lds = v_lds;
+  c.wave = threadIdx.x >> 6;
+  c.l = threadIdx.x & 63;
+  c.tt = c.l & 15;
+  c.sq = (c.wave << 2) | (c.l >> 4);
+  const int l = c.l, wave = c.wave;
+  auto window = [&](int grp, unsigned (&off)[16]) {
+    const int tile = grp * 16 + c.tt;
+    const int ty = tile / T2;
+    c.window(tile < TPB, N, 0, ty, tile - ty * T2, off);
+  };
+  auto out_pixel = [&](int grp) {
+    const int tile = grp * 16 + (l & 15), ty = tile / T2, tx = tile - ty * T2;
+    return tile < TPB ? (2 * ty) * N + 2 * tx : -1;
+  };
+  for (int layer = 0; layer < nlayers; ++layer) {
+    const float* in = layer == 0 ? x0 : ((layer & 1) ? hA : hB);
+    float* dst = layer + 1 == nlayers ? out : ((layer & 1) ? hB : hA);
+    const bool last = layer + 1 == nlayers, relu = last || !(layer & 1);
+    c.xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + board, 0, N * N * 256, 0x00020000);
+    const f32x4* usrc = reinterpret_cast<const f32x4*>(u2all + (size_t)layer * kW2UFloats) + (size_t)wave * 64 * kWave + l;
+    f32x4 ur[64];
+    f32x4 raw[16];
+    f32x4 bias4;
+    {
+      f32x4 raw0[16];
+      unsigned off[16];
+      window(0, off);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) raw0[q] = c.ld(off[q]);
+      window(NG > 1 ? 1 : 0, off);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) raw[q] = c.ld(off[q]);
+      bias4 = *reinterpret_cast<const f32x4*>(biasall + layer * 64 + 16 * wave + 4 * (l >> 4));
+      __builtin_amdgcn_sched_barrier(0);
+      w2_load_u01(ur, usrc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c.transform_part(raw0, 0, k);
+    }
+    __syncthreads();
+    auto group = [&](int grp, int buf, auto first) {
+      const int nxt = grp + 1 < NG ? grp + 1 : grp;
+      f32x4 acc[16];
+      w2_group<decltype(first)::value>(c, ur, raw, usrc, bias4, buf, [&](unsigned (&off)[16]) { window(nxt, off); },
+                                       acc);
+      c.epilogue(acc, out_pixel(grp), N, relu, last ? x0 + board : nullptr, dst + board);
+      __syncthreads();
+    };
+    group(0, 0, std::true_type{});
+    for (int grp = 1; grp < NG; ++grp) group(grp, grp & 1, std::false_type{});
+    // the layer's stores complete and visible to the workgroup before the next layer reads them
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    asm volatile("buffer_inv sc0" ::: "memory");
+  }
 }
 
 // BK_CONV_DIRECT=1 forces the direct form for every shape (tests compare the two);
@@ -784,6 +879,38 @@ int bk_wino_stamps_clear() {
 int bk_conv3x3_packed_floats(int cin) {
   // cin 64: the direct form's 9*64*64 operands, then the Winograd form's U (2 halves)
   return (cin == 4 || cin == 8) ? 9 * cin * kCout : cin == 64 ? 9 * 64 * kCout + 2 * kWinoHalf + kW2UFloats : -1;
+}
+
+int bk_tower_u_floats(void) { return kW2UFloats; }
+int bk_tower_supported(int N) { return N == 8 || N == 14 || N == 20; }
+
+int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
+                    float* hB, float* out, void* stream) {
+  BK_REQUIRE(x0 && u2all && biasall && hA && hB && out && B >= 0 && nlayers >= 1, "bad argument");
+  BK_REQUIRE(bk_tower_supported(N), "bk_resnet_tower: N must be 8, 14 or 20");
+  BK_REQUIRE(((uintptr_t)x0 & 15u) == 0 && ((uintptr_t)hA & 15u) == 0 && ((uintptr_t)hB & 15u) == 0 &&
+                 ((uintptr_t)out & 15u) == 0 && ((uintptr_t)u2all & 15u) == 0 && ((uintptr_t)biasall & 15u) == 0,
+             "bk_resnet_tower: 16-byte aligned buffers");
+  BK_REQUIRE((int64_t)N * N * 256 < (1ll << 31), "bk_resnet_tower: board too large");
+  if (B == 0) return BK_OK;
+  const int lds = (int)(sizeof(float) * 2 * kW2VBuf);
+  static bool attr = false;
+  if (!attr) {
+    const void* fns[3] = {(const void*)k_tower_wino<8>, (const void*)k_tower_wino<14>, (const void*)k_tower_wino<20>};
+    for (const void* fn : fns)
+      if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds), "hipFuncSetAttribute") !=
+          BK_OK)
+        return BK_EHIP;
+    attr = true;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 20)
+    hipLaunchKernelGGL(k_tower_wino<20>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
+  else if (N == 14)
+    hipLaunchKernelGGL(k_tower_wino<14>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
+  else
+    hipLaunchKernelGGL(k_tower_wino<8>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
+  return launch_check("k_tower_wino");
 }
 
 int bk_conv3x3_form(int N, int cin) { return cin == 64 && N % 2 == 0 && !direct_only() ? 1 : 0; }

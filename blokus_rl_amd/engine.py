@@ -65,6 +65,9 @@ _SIGS = {
     "bk_conv3x3_form": (_i, [_i, _i]),
     "bk_conv3x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),
     "bk_resnet_heads": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
+    "bk_tower_u_floats": (_i, []),
+    "bk_tower_supported": (_i, [_i]),
+    "bk_resnet_tower": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

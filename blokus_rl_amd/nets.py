@@ -247,6 +247,37 @@ def conv3x3(x: torch.Tensor, wpacked: torch.Tensor, bias: torch.Tensor, relu: bo
     return y
 
 
+def pack_tower(weights) -> torch.Tensor:
+    """[64, 64, 3, 3] weights of the tower's convs, in order -> bk_resnet_tower's u2all: each
+    layer's Winograd U in the form-2 register order (the tail of pack_winograd), concatenated."""
+    return torch.cat([pack_winograd(w)[-(4 * 64 * 64 * 4):] for w in weights]).contiguous()
+
+
+def tower_enabled() -> bool:
+    """BK_TOWER=0 runs the residual tower as one bk_conv3x3 launch per layer instead of the fused
+    bk_resnet_tower (same arithmetic; for comparisons)."""
+    import os
+
+    return os.environ.get("BK_TOWER", "1") != "0"
+
+
+def resnet_tower(x: torch.Tensor, u2all: torch.Tensor, biasall: torch.Tensor, nlayers: int) -> torch.Tensor:
+    """bk_resnet_tower: x = the stem output [B, 64, N, N] channels_last -> relu(x + tower(x))."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, C, N, _ = x.shape
+    assert C == 64 and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+    lib = load_library()
+    assert u2all.numel() == nlayers * lib.bk_tower_u_floats() and biasall.numel() == nlayers * 64
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    ha = torch.empty_like(x, memory_format=torch.channels_last)
+    hb = torch.empty_like(x, memory_format=torch.channels_last)
+    _check(lib.bk_resnet_tower(ctypes.c_void_p(x.data_ptr()), B, N, nlayers, _ptr(u2all), _ptr(biasall),
+                               ctypes.c_void_p(ha.data_ptr()), ctypes.c_void_p(hb.data_ptr()),
+                               ctypes.c_void_p(out.data_ptr()), _stream(x.device)))
+    return out
+
+
 def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
     """bk_resnet_heads: tower output [B, 64, N, N] channels_last -> (policy features [B, 2*N*N] in
     the NCHW flatten order, values [B, P])."""
@@ -267,9 +298,10 @@ def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
 
 
 class LeafResNet(nn.Module):
-    """The leaf evaluator's ResNet on the device (fp32): FusedResNet's function with every 3x3
-    conv + bias + ReLU (+ the tower's residual) as one bk_conv3x3 launch (fp32 MFMA, weights
-    resident in LDS, NHWC activations), both heads' 1x1 convs and the whole value MLP
+    """The leaf evaluator's ResNet on the device (fp32): FusedResNet's function with the stem conv +
+    bias + ReLU as one bk_conv3x3 launch, the whole residual tower (Winograd fp32 MFMA, NHWC
+    activations; + the tower's residual and ReLU) as one bk_resnet_tower launch (board sizes it
+    supports; one bk_conv3x3 launch per conv otherwise), both heads' 1x1 convs and the whole value MLP
     in one bk_resnet_heads launch, and the policy Linear in hipBLASLt (or, features=True, left to
     the search's sparse head). Input: the planar observation [B, 2P, N, N]. With normalize=False the policy
     comes back as raw logits (the leaf batch's consumer, k_expand_backup, takes a softmax over the
@@ -287,6 +319,10 @@ class LeafResNet(nn.Module):
             for i, (c1, c2) in enumerate(f.blocks):
                 self.register_buffer(f"w_{i}_1", pack_conv3x3(c1.weight.detach()))
                 self.register_buffer(f"w_{i}_2", pack_conv3x3(c2.weight.detach()))
+            if len(f.blocks):  # the fused tower's operands (bk_resnet_tower)
+                convs = [c for blk in f.blocks for c in blk]
+                self.register_buffer("u_tower", pack_tower([c.weight.detach() for c in convs]))
+                self.register_buffer("b_tower", torch.cat([c.bias.detach().float() for c in convs]).contiguous())
 
     @torch.no_grad()
     def forward(self, x):
@@ -296,9 +332,14 @@ class LeafResNet(nn.Module):
             # planar observation in (as the search writes it), NHWC activations through the tower
             x = conv3x3(x.float().contiguous(), self.w_stem, f.stem.bias, True)
             h = x
-            for i, (c1, c2) in enumerate(f.blocks):
-                h = conv3x3(h, getattr(self, f"w_{i}_1"), c1.bias, True)
-                h = conv3x3(h, getattr(self, f"w_{i}_2"), c2.bias, i + 1 == n, x if i + 1 == n else None)
+            from .engine import load_library
+
+            if n and tower_enabled() and load_library().bk_tower_supported(x.shape[2]):
+                h = resnet_tower(x, self.u_tower, self.b_tower, 2 * n)
+            else:
+                for i, (c1, c2) in enumerate(f.blocks):
+                    h = conv3x3(h, getattr(self, f"w_{i}_1"), c1.bias, True)
+                    h = conv3x3(h, getattr(self, f"w_{i}_2"), c2.bias, i + 1 == n, x if i + 1 == n else None)
             if not n:
                 h = torch.relu(x + x)
             pf, v = resnet_heads(h, f)

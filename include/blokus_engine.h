@@ -260,6 +260,16 @@ int bk_resnet_heads(const float* x, int B, int NN, const float* wp, const float*
                     float* vout, void* stream);
 int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, const float* bias, const float* residual,
                int relu, float* y, void* stream);
+/* The whole residual tower of the inference ResNet (blokus_nnet.py:140-141 with the block
+ * structure of :103-112, BN folded) in one launch, one workgroup per board: nlayers = 2 x blocks
+ * 3x3 convs 64->64, ReLU after each block's first conv, out = relu(x0 + tower(x0)). x0, hA, hB, out
+ * are NHWC [B][N][N][64] (hA, hB scratch); u2all [nlayers][bk_tower_u_floats()] holds each layer's
+ * Winograd U in the form-2 register order (nets.py pack_tower), biasall [nlayers][64].
+ * Supported N: 8, 14, 20 (bk_tower_supported). Same arithmetic as nlayers bk_conv3x3 calls. */
+int bk_tower_u_floats(void);
+int bk_tower_supported(int N);
+int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
+                    float* hB, float* out, void* stream);
 
 #ifdef __cplusplus
 }

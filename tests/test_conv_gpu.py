@@ -127,3 +127,32 @@ def test_leaf_resnet_raw_logits_give_same_masked_softmax():
     a = torch.softmax(lp[:, ids], 1)
     b = torch.softmax(lg[:, ids], 1)
     assert (a - b).abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("B,N,nblocks", [(256, 20, 5), (3, 20, 2), (300, 20, 1), (37, 14, 2), (5, 8, 3)])
+def test_resnet_tower_matches_per_layer_convs(B, N, nblocks):
+    """bk_resnet_tower (the whole tower in one launch, one workgroup per board) does the same
+    arithmetic as the chain of per-layer Winograd form-2 bk_conv3x3 launches: bitwise equal; and
+    within the f32 bound of an fp64 torch tower."""
+    from blokus_rl_amd.engine import load_library
+    from blokus_rl_amd.nets import conv3x3, pack_conv3x3, pack_tower, resnet_tower
+
+    assert load_library().bk_tower_supported(N)
+    g = torch.Generator(device="cuda").manual_seed(B + N + nblocks)
+    x = torch.relu(torch.randn((B, 64, N, N), device="cuda", generator=g)).contiguous(memory_format=torch.channels_last)
+    ws = [torch.randn((64, 64, 3, 3), device="cuda", generator=g) / 24 for _ in range(2 * nblocks)]
+    bs = [torch.randn(64, device="cuda", generator=g) * 0.1 for _ in range(2 * nblocks)]
+    out = resnet_tower(x, pack_tower(ws), torch.cat(bs).contiguous(), 2 * nblocks)
+    h = x
+    for i in range(2 * nblocks):
+        last = i + 1 == 2 * nblocks
+        h = conv3x3(h, pack_conv3x3(ws[i]), bs[i], last or i % 2 == 0, x if last else None)
+    torch.cuda.synchronize()
+    assert torch.equal(out, h)
+    ref = x.double()
+    for i in range(2 * nblocks):
+        ref = F.conv2d(ref, ws[i].double(), bs[i].double(), padding=1)
+        if i % 2 == 0:
+            ref = torch.relu(ref)
+    ref = torch.relu(ref + x.double())
+    assert float((out.double() - ref).abs().max()) <= 1e-4 * (float(ref.abs().max()) + 1.0)
