@@ -588,9 +588,12 @@ struct W2Lane {
     *reinterpret_cast<f32x2*>(dst + (4 * i + 3) * 64) = pk_sub(t[1], t[3]);
   }
   // A^T M A + residual + ReLU of the lane's tile (top-left output pixel opix, -1 = none) for
-  // channels 16 wave + 4 (l >> 4) + 0..3, on packed channel pairs; y / res point at pixel 0 of
-  // their [..][N][N][64] buffers
-  __device__ void epilogue(const f32x4 (&acc)[16], int opix, int N, bool relu, const float* res, float* y) const {
+  // channels 16 wave + 4 (l >> 4) + 0..3, on packed channel pairs; y / res: buffer resources whose
+  // byte 0 is pixel 0 of their [..][N][N][64] buffers (buffer stores/loads: the destination may be
+  // chosen at run time without turning the accesses into flat ones)
+  template <bool RELU, bool RES>
+  __device__ void epilogue(const f32x4 (&acc)[16], int opix, int N, __amdgpu_buffer_rsrc_t res,
+                           __amdgpu_buffer_rsrc_t y) const {
     if (opix < 0) return;
     f32x2 yv[4][2];  // [pixel 2i + j][pair h]
 #pragma unroll
@@ -610,24 +613,72 @@ struct W2Lane {
     }
 #pragma unroll
     for (int px = 0; px < 4; ++px) {
-      const size_t o = (size_t)(opix + (px >> 1) * N + (px & 1)) * 64 + 16 * wave + 4 * (l >> 4);
+      const unsigned o = ((unsigned)(opix + (px >> 1) * N + (px & 1)) * 64 + 16 * wave + 4 * (l >> 4)) * 4;
       f32x2 lo = yv[px][0], hi = yv[px][1];
-      if (res) {
-        const f32x4 rr = *reinterpret_cast<const f32x4*>(res + o);
+      if (RES) {
+        const f32x4 rr = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(res, o, 0, 0));
         lo = pk_add(lo, rr.xy);
         hi = pk_add(hi, rr.zw);
       }
       f32x4 out = f32x4{lo.x, lo.y, hi.x, hi.y};
-      if (relu) {
+      if (RELU) {
         out.x = fmaxf(out.x, 0.0f);
         out.y = fmaxf(out.y, 0.0f);
         out.z = fmaxf(out.z, 0.0f);
         out.w = fmaxf(out.w, 0.0f);
       }
-      *reinterpret_cast<f32x4*>(y + o) = out;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out), y,
+                                             o, 0, 0);
     }
   }
 };
+
+// the fused tower's epilogue: ReLU as data (max with floor: 0, or -inf for none), the residual
+// (RES, the tower's last conv) from res
+template <bool RES>
+__device__ __forceinline__ void w2_epilogue_flags(const W2Lane& c, const f32x4 (&acc)[16], int opix, int N,
+                                                  float floor, __amdgpu_buffer_rsrc_t res,
+                                                  __amdgpu_buffer_rsrc_t y) {
+  if (opix < 0) return;
+  f32x2 yv[4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    auto m = [&](int q) { return h ? acc[q].zw : acc[q].xy; };
+    f32x2 u2v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u2v[j] = pk_add(pk_add(m(j), m(4 + j)), m(8 + j));
+      u2v[4 + j] = pk_sub(pk_sub(m(4 + j), m(8 + j)), m(12 + j));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      yv[2 * i][h] = pk_add(pk_add(u2v[4 * i + 0], u2v[4 * i + 1]), u2v[4 * i + 2]);
+      yv[2 * i + 1][h] = pk_sub(pk_sub(u2v[4 * i + 1], u2v[4 * i + 2]), u2v[4 * i + 3]);
+    }
+  }
+#pragma unroll
+  for (int px = 0; px < 4; ++px) {
+    const unsigned o = ((unsigned)(opix + (px >> 1) * N + (px & 1)) * 64 + 16 * c.wave + 4 * (c.l >> 4)) * 4;
+    f32x2 lo = yv[px][0], hi = yv[px][1];
+    if (RES) {
+      const f32x4 rr = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(res, o, 0, 0));
+      lo = pk_add(lo, rr.xy);
+      hi = pk_add(hi, rr.zw);
+    }
+    const f32x4 out = f32x4{fmaxf(lo.x, floor), fmaxf(lo.y, floor), fmaxf(hi.x, floor), fmaxf(hi.y, floor)};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out), y, o,
+                                           0, 0);
+  }
+}
+
+// a buffer resource over [p, p + bytes) with its base made provably wave-uniform (readfirstlane),
+// so selecting p at run time never makes hipcc wrap the buffer ops in waterfall loops
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t w2_rsrc(const float* p, int bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  const uintptr_t u = ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, bytes, 0x00020000);
+}
 
 // The first group's U: this wave's k-steps 0 and 1 (the rest stream in under the first group's
 // MFMAs, w2_group<true>), in k-step order, ur[4s + p/4][p%4] = U[16 wave + (l & 15)][4s + (l >> 4)][p]
@@ -642,14 +693,19 @@ __device__ __forceinline__ void w2_load_u01(f32x4 (&ur)[64], const f32x4* usrc) 
 // One group of 16 tiles, V already in LDS buffer buf: 16 k-steps of 16 MFMAs (A = U from AGPRs
 // via inline asm, B = V from LDS one step ahead, accumulators in VGPRs, the bias as the initial
 // accumulator of position (1,1)); meanwhile the next group's window loads go out over steps 0-3
-// (offsets from next_window() at step 0; FIRST: already in raw) and its transform runs in 8 parts
-// over steps 8-15 into V[buf ^ 1]; FIRST also loads U two k-steps ahead. f32 MFMAs run on the
-// SIMD's vector ALUs, so a VALU instruction beside them is not hidden and every MFMA <-> VALU
-// switch costs ~10 cycles (tools/probe/mfma_fill.hip): the MFMA stream carries no VALU, and the
-// VALU work comes in batches. Returns with acc ready for the epilogue.
-template <bool FIRST, class NextWindow>
+// (offsets from next_window() at step 0, through buffer xr_next) and its transform runs in 8
+// parts over steps 8-15 into V[buf ^ 1]. MODE kW2First: this group streams its own U in two
+// k-steps ahead (k-steps 0, 1 are loaded before it); in the per-layer kernel the next window is
+// already in raw (the prologue loaded it). MODE kW2Last (a layer's last group in the fused
+// tower): after the MFMAs, U of the next layer's k-steps 0, 1 (unext). f32 MFMAs run on the SIMD's vector
+// ALUs, so a VALU instruction beside them is not hidden and every MFMA <-> VALU switch costs ~10
+// cycles (tools/probe/mfma_fill.hip): the MFMA stream carries no VALU, and the VALU work comes
+// in batches. Returns with acc ready for the epilogue.
+constexpr int kW2Mid = 0, kW2First = 1, kW2Last = 2;
+template <int MODE, bool WINDOW_IN_RAW = (MODE == kW2First), class NextWindow>
 __device__ __forceinline__ void w2_group(const W2Lane& c, f32x4 (&ur)[64], f32x4 (&raw)[16], const f32x4* usrc,
-                                         f32x4 bias4, int buf, NextWindow next_window, f32x4 (&acc)[16]) {
+                                         const f32x4* unext, __amdgpu_buffer_rsrc_t xr_next, f32x4 bias4, int buf,
+                                         NextWindow next_window, f32x4 (&acc)[16]) {
   const float* vsrc = c.v_lds + buf * kW2VBuf + (c.l & 15) * 4 + (c.l >> 4);  // V[buf][s][p][t][g]
   float vb[2][16];
   unsigned off[16];
@@ -657,12 +713,13 @@ __device__ __forceinline__ void w2_group(const W2Lane& c, f32x4 (&ur)[64], f32x4
   for (int p = 0; p < 16; ++p) vb[0][p] = vsrc[p * 64];
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    if (s == 0 && !FIRST) next_window(off);
-    if (s < 4 && !FIRST) {
+    if (s == 0 && !WINDOW_IN_RAW) next_window(off);
+    if (s < 4 && !WINDOW_IN_RAW) {
 #pragma unroll
-      for (int q = 4 * s; q < 4 * s + 4; ++q) raw[q] = c.ld(off[q]);
+      for (int q = 4 * s; q < 4 * s + 4; ++q)
+        raw[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr_next, off[q], 0, 0));
     }
-    if (FIRST && s + 2 < 16) {  // U of k-step s + 2, in order
+    if (MODE == kW2First && s + 2 < 16) {  // U of k-step s + 2, in order
 #pragma unroll
       for (int q = 4 * (s + 2); q < 4 * (s + 2) + 4; ++q) {
         ur[q] = usrc[q * kWave];
@@ -689,6 +746,7 @@ __device__ __forceinline__ void w2_group(const W2Lane& c, f32x4 (&ur)[64], f32x4
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (MODE == kW2Last) w2_load_u01(ur, unext);  // the next layer's first group streams in the rest
   // the accumulators are written by MFMAs the compiler cannot see: wait out the XDL write ->
   // VALU read latency before the epilogue reads them
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -761,10 +819,10 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __
     W2STAMP(2 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
     const int nxt = grp + 1 < c_hi ? grp + 1 : grp;
     f32x4 acc[16];
-    w2_group<decltype(first)::value>(c, ur, raw, usrc, bias4, buf, [&](unsigned (&off)[16]) { window(nxt, off); },
-                                     acc);
+    w2_group<decltype(first)::value ? kW2First : kW2Mid>(c, ur, raw, usrc, usrc, c.xr, bias4, buf,
+                                                          [&](unsigned (&off)[16]) { window(nxt, off); }, acc);
     W2STAMP(3 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
-    c.epilogue(acc, out_pixel(grp), N, RELU, RES ? res : nullptr, y);
+    c.epilogue<RELU, RES>(acc, out_pixel(grp), N, w2_rsrc(RES ? res : y, tiles * 1024), w2_rsrc(y, tiles * 1024));
     __syncthreads();  // V[buf ^ 1] complete for the next group; V[buf] free to be overwritten
     W2STAMP(4 + 3 * (grp - c_lo), __builtin_amdgcn_s_memtime());
   };
@@ -779,72 +837,167 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_conv3x3_wino2(const float* __
 // launch, one workgroup per board: layer l = conv3x3 (Winograd form 2) over the board, ReLU on
 // even layers (each block's first conv), the last layer adds the tower input and takes the ReLU;
 // intermediate activations ping-pong between hA and hB. A board's tiles depend only on the same
-// board, so layers are separated by a workgroup barrier instead of a kernel boundary: no launch
-// gap, no cold L2 after a cross-XCD release, and the next layer's first windows are L2-hot.
+// board, so there is no kernel boundary between layers (no launch gap, no cold L2 after a
+// cross-XCD release): the (layer, group) pairs run as one pipeline, each pair loading and
+// transforming the NEXT pair's window, across layer boundaries too. That is safe because a window
+// only reads rows its layer's predecessor finished at least two pairs earlier (tower_pipeline_ok),
+// and a wave's wait for its window loads also waits for all its older stores, so after a group
+// barrier every store of two pairs back is complete. A layer's last group refills the U registers
+// with the next layer's U step by step (and invalidates L1 before loading next-layer windows).
+template <int N>
+constexpr bool tower_pipeline_ok() {
+  constexpr int T2 = N / 2, TPB = T2 * T2, NG = (TPB + 15) / 16;
+  if (NG < 3) return false;
+  // the window of group k (tiles 16k..16k+15) reads output rows up to 2*ty_max + 2 of the previous
+  // layer, i.e. its tiles up to (ty_max + 1) * T2 + T2 - 1: their group must be <= k + NG - 2
+  // (two pairs before the pair that issues the loads, pair (layer, k) - 1)
+  for (int k = 0; k < NG; ++k) {
+    const int last_tile = 16 * k + 15 < TPB ? 16 * k + 15 : TPB - 1;
+    int ty = last_tile / T2 + 1;
+    if (ty > T2 - 1) ty = T2 - 1;
+    const int need = (ty * T2 + T2 - 1) / 16;  // previous layer's group
+    if (need > k + NG - 3) return false;
+  }
+  return true;
+}
+
+// Board-level state of k_tower_wino (plain struct + force-inlined functions: nested lambdas around
+// the 256-register U array defeat hipcc's promotion of it to AGPRs)
+template <int N>
+struct Tower {
+  static constexpr int T2 = N / 2, TPB = T2 * T2, NG = (TPB + 15) / 16;
+  W2Lane c;
+  uintptr_t a_x0, a_a, a_b, a_out;  // the board's base in each activation buffer (integers: a select
+                                    // among pointers would make hipcc assume they may alias U)
+  const float* u2all;
+  const float* biasall;
+  int nlayers;
+  __device__ static __amdgpu_buffer_rsrc_t rsrc(uintptr_t a, int bytes) { return w2_rsrc((const float*)a, bytes); }
+  // selections by bit masks (hipcc turns a select chain into a lookup table in scratch memory)
+  __device__ static uintptr_t pick(bool c, uintptr_t a, uintptr_t b) {
+    const uintptr_t m = (uintptr_t)0 - (uintptr_t)c;
+    return (a & m) | (b & ~m);
+  }
+  __device__ __amdgpu_buffer_rsrc_t in_of(int layer) const {
+    return rsrc(pick(layer == 0, a_x0, pick(layer & 1, a_a, a_b)), N * N * 256);
+  }
+  __device__ __amdgpu_buffer_rsrc_t out_of(int layer) const {
+    return rsrc(pick(layer + 1 == nlayers, a_out, pick(layer & 1, a_b, a_a)), N * N * 256);
+  }
+  __device__ __amdgpu_buffer_rsrc_t res_of(int layer) const {  // the last layer's residual; 0s otherwise
+    return rsrc(a_x0, layer + 1 == nlayers ? N * N * 256 : 0);
+  }
+  __device__ const f32x4* u_of(int layer) const {
+    return reinterpret_cast<const f32x4*>(u2all + (size_t)layer * kW2UFloats) + (size_t)c.wave * 64 * kWave + c.l;
+  }
+  __device__ f32x4 bias_of(int layer) const {
+    return *reinterpret_cast<const f32x4*>(biasall + layer * 64 + 16 * c.wave + 4 * (c.l >> 4));
+  }
+  __device__ void window(int grp, unsigned (&off)[16]) const {
+    const int tile = grp * 16 + c.tt, ty = tile / T2;
+    c.window(tile < TPB, N, 0, ty, tile - ty * T2, off);
+  }
+  __device__ int out_pixel(int grp) const {
+    const int tile = grp * 16 + (c.l & 15), ty = tile / T2, tx = tile - ty * T2;
+    return tile < TPB ? (2 * ty) * N + 2 * tx : -1;
+  }
+};
+
+// One (layer, group) pair of the tower pipeline, MODE kW2First / kW2Mid / kW2Last (a layer's last
+// group: the next pair is (layer + 1, 0) and U is refilled with the next layer's)
+template <int M, bool WINDOW_IN_RAW, int N>
+__device__ __forceinline__ void tower_pair(const Tower<N>& t, f32x4 (&ur)[64], f32x4 (&raw)[16], f32x4& bias4,
+                                           int layer, int grp) {
+  const bool last = layer + 1 == t.nlayers, relu = last || !(layer & 1);
+  // the next pair: (layer, grp + 1), or (layer + 1, 0) after a layer's last group (the last pair of
+  // the tower re-reads its own window into the idle V buffer: unconditional work)
+  const bool cross = M == kW2Last && !last;
+  const int nl = cross ? layer + 1 : layer, ng = M == kW2Last ? (last ? grp : 0) : grp + 1;
+  if (M == kW2Last) asm volatile("buffer_inv sc0" ::: "memory");  // next-layer windows: no stale L1 lines
+  f32x4 acc[16];
+  w2_group<M, WINDOW_IN_RAW>(t.c, ur, raw, t.u_of(layer), t.u_of(nl), t.in_of(nl), bias4, (layer * Tower<N>::NG + grp) & 1,
+              [&](unsigned (&off)[16]) { t.window(ng, off); }, acc);
+#if BK_WINO_STAMP
+  const int l = t.c.l, wave = t.c.wave;
+  if (layer == 2) W2STAMP(10 + grp, __builtin_amdgcn_s_memtime());
+#endif
+  if (last)  // the tower's last conv: + the tower input (a uniform branch)
+    w2_epilogue_flags<true>(t.c, acc, t.out_pixel(grp), N, 0.0f, t.res_of(layer), t.out_of(layer));
+  else
+    w2_epilogue_flags<false>(t.c, acc, t.out_pixel(grp), N, relu ? 0.0f : -__builtin_inff(), t.res_of(layer),
+                             t.out_of(layer));
+  if (M == kW2Last) {
+    bias4 = t.bias_of(nl);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load pending across the layer loop's back edge
+  }
+  __syncthreads();  // V[buf ^ 1] complete for the next pair; V[buf] free to be overwritten
+#if BK_WINO_STAMP
+  if (layer == 2) W2STAMP(3 + grp, __builtin_amdgcn_s_memtime());
+#endif
+}
+
 template <int N>
 __global__ __launch_bounds__(kW2Threads, 1) void k_tower_wino(const float* __restrict__ x0, float* hA, float* hB,
                                                               float* __restrict__ out,
                                                               const float* __restrict__ u2all,
                                                               const float* __restrict__ biasall, int nlayers) {
   extern __shared__ __attribute__((aligned(16))) float v_lds[];  // [2 buf][16 s][16 p][16 t][4 g]
-  constexpr int T2 = N / 2, TPB = T2 * T2, NG = (TPB + 15) / 16;
+  static_assert(tower_pipeline_ok<N>(), "k_tower_wino: board too small for the cross-layer pipeline");
+  constexpr int NG = Tower<N>::NG;
   const size_t board = (size_t)blockIdx.x * N * N * 64;
-  W2Lane c;
-  c.v_lds = v_lds;
-  c.wave = threadIdx.x >> 6;
-  c.l = threadIdx.x & 63;
-  c.tt = c.l & 15;
-  c.sq = (c.wave << 2) | (c.l >> 4);
-  const int l = c.l, wave = c.wave;
-  auto window = [&](int grp, unsigned (&off)[16]) {
-    const int tile = grp * 16 + c.tt;
-    const int ty = tile / T2;
-    c.window(tile < TPB, N, 0, ty, tile - ty * T2, off);
-  };
-  auto out_pixel = [&](int grp) {
-    const int tile = grp * 16 + (l & 15), ty = tile / T2, tx = tile - ty * T2;
-    return tile < TPB ? (2 * ty) * N + 2 * tx : -1;
-  };
-  for (int layer = 0; layer < nlayers; ++layer) {
-    const float* in = layer == 0 ? x0 : ((layer & 1) ? hA : hB);
-    float* dst = layer + 1 == nlayers ? out : ((layer & 1) ? hB : hA);
-    const bool last = layer + 1 == nlayers, relu = last || !(layer & 1);
-    c.xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + board, 0, N * N * 256, 0x00020000);
-    const f32x4* usrc = reinterpret_cast<const f32x4*>(u2all + (size_t)layer * kW2UFloats) + (size_t)wave * 64 * kWave + l;
-    f32x4 ur[64];
-    f32x4 raw[16];
-    f32x4 bias4;
-    {
-      f32x4 raw0[16];
-      unsigned off[16];
-      window(0, off);
+  Tower<N> t;
+  t.c.v_lds = v_lds;
+  t.c.wave = threadIdx.x >> 6;
+  t.c.l = threadIdx.x & 63;
+  t.c.tt = t.c.l & 15;
+  t.c.sq = (t.c.wave << 2) | (t.c.l >> 4);
+  const int l = t.c.l, wave = t.c.wave;
+  W2STAMP(0, __builtin_amdgcn_s_memtime());
+  W2STAMP(30, __builtin_amdgcn_s_memrealtime());
+  // buffer resources of the board in each activation buffer, built once (selecting among
+  // resources, never among pointers, keeps every access a buffer op on a uniform descriptor)
+  t.a_x0 = (uintptr_t)(x0 + board);
+  t.a_a = (uintptr_t)(hA + board);
+  t.a_b = (uintptr_t)(hB + board);
+  t.a_out = (uintptr_t)(out + board);
+  t.u2all = u2all;
+  t.biasall = biasall;
+  t.nlayers = nlayers;
+  t.c.xr = t.in_of(0);
+  // prologue: windows of pairs (0, 0) and (0, 1), layer 0's bias and U of k-steps 0, 1
+  f32x4 ur[64];
+  f32x4 raw[16];
+  f32x4 bias4;
+  {
+    f32x4 raw0[16];
+    unsigned off[16];
+    t.window(0, off);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) raw0[q] = c.ld(off[q]);
-      window(NG > 1 ? 1 : 0, off);
+    for (int q = 0; q < 16; ++q) raw0[q] = t.c.ld(off[q]);
+    t.window(1, off);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) raw[q] = c.ld(off[q]);
-      bias4 = *reinterpret_cast<const f32x4*>(biasall + layer * 64 + 16 * wave + 4 * (l >> 4));
-      __builtin_amdgcn_sched_barrier(0);
-      w2_load_u01(ur, usrc);
+    for (int q = 0; q < 16; ++q) raw[q] = t.c.ld(off[q]);
+    bias4 = t.bias_of(0);
+    __builtin_amdgcn_sched_barrier(0);
+    w2_load_u01(ur, t.u_of(0));
 #pragma unroll
-      for (int k = 0; k < 8; ++k) c.transform_part(raw0, 0, k);
-    }
-    __syncthreads();
-    auto group = [&](int grp, int buf, auto first) {
-      const int nxt = grp + 1 < NG ? grp + 1 : grp;
-      f32x4 acc[16];
-      w2_group<decltype(first)::value>(c, ur, raw, usrc, bias4, buf, [&](unsigned (&off)[16]) { window(nxt, off); },
-                                       acc);
-      c.epilogue(acc, out_pixel(grp), N, relu, last ? x0 + board : nullptr, dst + board);
-      __syncthreads();
-    };
-    group(0, 0, std::true_type{});
-    for (int grp = 1; grp < NG; ++grp) group(grp, grp & 1, std::false_type{});
-    // the layer's stores complete and visible to the workgroup before the next layer reads them
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    __syncthreads();
-    asm volatile("buffer_inv sc0" ::: "memory");
+    for (int k = 0; k < 8; ++k) t.c.transform_part(raw0, 0, k);
   }
+  __syncthreads();
+  W2STAMP(1, __builtin_amdgcn_s_memtime());
+  tower_pair<kW2First, true>(t, ur, raw, bias4, 0, 0);
+  for (int grp = 1; grp < NG - 1; ++grp) tower_pair<kW2Mid, false>(t, ur, raw, bias4, 0, grp);
+  tower_pair<kW2Last, false>(t, ur, raw, bias4, 0, NG - 1);
+  for (int layer = 1; layer < nlayers; ++layer) {
+    tower_pair<kW2First, false>(t, ur, raw, bias4, layer, 0);
+    for (int grp = 1; grp < NG - 1; ++grp) tower_pair<kW2Mid, false>(t, ur, raw, bias4, layer, grp);
+    tower_pair<kW2Last, false>(t, ur, raw, bias4, layer, NG - 1);
+    if (layer == 2) W2STAMP(2, __builtin_amdgcn_s_memtime());
+  }
+  W2STAMP(29, __builtin_amdgcn_s_memtime());
+  W2STAMP(31, __builtin_amdgcn_s_memrealtime());
+  (void)l;
+  (void)wave;
 }
 
 // BK_CONV_DIRECT=1 forces the direct form for every shape (tests compare the two);
@@ -882,12 +1035,12 @@ int bk_conv3x3_packed_floats(int cin) {
 }
 
 int bk_tower_u_floats(void) { return kW2UFloats; }
-int bk_tower_supported(int N) { return N == 8 || N == 14 || N == 20; }
+int bk_tower_supported(int N) { return N == 14 || N == 20; }
 
 int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
                     float* hB, float* out, void* stream) {
   BK_REQUIRE(x0 && u2all && biasall && hA && hB && out && B >= 0 && nlayers >= 1, "bad argument");
-  BK_REQUIRE(bk_tower_supported(N), "bk_resnet_tower: N must be 8, 14 or 20");
+  BK_REQUIRE(bk_tower_supported(N), "bk_resnet_tower: N must be 14 or 20");
   BK_REQUIRE(((uintptr_t)x0 & 15u) == 0 && ((uintptr_t)hA & 15u) == 0 && ((uintptr_t)hB & 15u) == 0 &&
                  ((uintptr_t)out & 15u) == 0 && ((uintptr_t)u2all & 15u) == 0 && ((uintptr_t)biasall & 15u) == 0,
              "bk_resnet_tower: 16-byte aligned buffers");
@@ -896,7 +1049,7 @@ int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2a
   const int lds = (int)(sizeof(float) * 2 * kW2VBuf);
   static bool attr = false;
   if (!attr) {
-    const void* fns[3] = {(const void*)k_tower_wino<8>, (const void*)k_tower_wino<14>, (const void*)k_tower_wino<20>};
+    const void* fns[2] = {(const void*)k_tower_wino<14>, (const void*)k_tower_wino<20>};
     for (const void* fn : fns)
       if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds), "hipFuncSetAttribute") !=
           BK_OK)
@@ -906,10 +1059,8 @@ int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2a
   hipStream_t s = (hipStream_t)stream;
   if (N == 20)
     hipLaunchKernelGGL(k_tower_wino<20>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
-  else if (N == 14)
-    hipLaunchKernelGGL(k_tower_wino<14>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
   else
-    hipLaunchKernelGGL(k_tower_wino<8>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
+    hipLaunchKernelGGL(k_tower_wino<14>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
   return launch_check("k_tower_wino");
 }
 

@@ -265,7 +265,7 @@ int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, cons
  * 3x3 convs 64->64, ReLU after each block's first conv, out = relu(x0 + tower(x0)). x0, hA, hB, out
  * are NHWC [B][N][N][64] (hA, hB scratch); u2all [nlayers][bk_tower_u_floats()] holds each layer's
  * Winograd U in the form-2 register order (nets.py pack_tower), biasall [nlayers][64].
- * Supported N: 8, 14, 20 (bk_tower_supported). Same arithmetic as nlayers bk_conv3x3 calls. */
+ * Supported N: 14, 20 (bk_tower_supported). Same arithmetic as nlayers bk_conv3x3 calls. */
 int bk_tower_u_floats(void);
 int bk_tower_supported(int N);
 int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,

@@ -129,7 +129,7 @@ def test_leaf_resnet_raw_logits_give_same_masked_softmax():
     assert (a - b).abs().max().item() < 1e-6
 
 
-@pytest.mark.parametrize("B,N,nblocks", [(256, 20, 5), (3, 20, 2), (300, 20, 1), (37, 14, 2), (5, 8, 3)])
+@pytest.mark.parametrize("B,N,nblocks", [(256, 20, 5), (3, 20, 2), (300, 20, 1), (37, 14, 2), (5, 14, 3)])
 def test_resnet_tower_matches_per_layer_convs(B, N, nblocks):
     """bk_resnet_tower (the whole tower in one launch, one workgroup per board) does the same
     arithmetic as the chain of per-layer Winograd form-2 bk_conv3x3 launches: bitwise equal; and
