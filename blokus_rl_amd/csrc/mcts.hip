@@ -261,8 +261,8 @@ __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const ui
 // expansion reads): logit[j] = W[id_j] . feat[t] + bias[id_j] for the K legal ids of tree t's
 // leaf, instead of the dense [T, A] Linear (blokus_nnet.py:147-148) — K ~ 200 of A = 30433.
 // kLeafBlocks workgroups per tree each compact the leaf bitmask (ascending ids) and take a
-// contiguous share of the ids; a wave computes one dot product at a time over the feature row
-// staged in LDS, W rows read as coalesced float4s.
+// contiguous share of the ids; a wave computes four dot products at a time (16 lanes each) over
+// the feature row staged in LDS, W rows read as coalesced float4s, several loads in flight.
 __global__ __launch_bounds__(256) void k_leaf_logits(DevPreset dp, DevMcts m, const float* __restrict__ feat,
                                                      int64_t ldf, int F, const float* __restrict__ W,
                                                      const float* __restrict__ bias) {
@@ -299,30 +299,36 @@ __global__ __launch_bounds__(256) void k_leaf_logits(DevPreset dp, DevMcts m, co
   float* out_lg = m.leaf_logit + (size_t)t * kLeafCap;
   const int nw = blockDim.x >> 6;
   if ((F & 3) == 0) {
+    // four ids per wave at a time, 16 lanes each: a lane streams every 16th float4 of its row
+    // (up to 4 loads in flight), the 16-lane partial sums meet in 4 xor-shuffles
     const int F4 = F >> 2;
     const float4* f4 = reinterpret_cast<const float4*>(f);
-    for (int j = lo + wave; j < hi; j += 2 * nw) {
-      // two ids per pass: both rows' loads in flight together
-      const int j2 = j + nw;
-      const int id = ids[j];
-      const int id2 = j2 < hi ? ids[j2] : id;
-      const float4* r1 = reinterpret_cast<const float4*>(W + (size_t)id * F);
-      const float4* r2 = reinterpret_cast<const float4*>(W + (size_t)id2 * F);
-      float a1 = 0.f, a2 = 0.f;
-      for (int q = l; q < F4; q += kWave) {
-        const float4 w1 = r1[q], w2 = r2[q], x = f4[q];
-        a1 += w1.x * x.x + w1.y * x.y + w1.z * x.z + w1.w * x.w;
-        a2 += w2.x * x.x + w2.y * x.y + w2.z * x.z + w2.w * x.w;
+    const int sub = l & 15, quad = l >> 4;
+    for (int j0 = lo + 4 * wave; j0 < hi; j0 += 4 * nw) {
+      const int j = j0 + quad;
+      const bool ok = j < hi;
+      const int id = ids[ok ? j : lo];
+      const float4* r = reinterpret_cast<const float4*>(W + (size_t)id * F);
+      float a0 = 0.f, a1 = 0.f;
+      int q = sub;
+      for (; q + 48 < F4; q += 64) {
+        const float4 w0 = r[q], w1 = r[q + 16], w2 = r[q + 32], w3 = r[q + 48];
+        const float4 x0 = f4[q], x1 = f4[q + 16], x2 = f4[q + 32], x3 = f4[q + 48];
+        a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
+        a1 += w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
+        a0 += w2.x * x2.x + w2.y * x2.y + w2.z * x2.z + w2.w * x2.w;
+        a1 += w3.x * x3.x + w3.y * x3.y + w3.z * x3.z + w3.w * x3.w;
       }
-      a1 = wave_sum_f(a1);
-      a2 = wave_sum_f(a2);
-      if (l == 0) {
+      for (; q < F4; q += 16) {
+        const float4 w0 = r[q], x0 = f4[q];
+        a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
+      }
+      float a = a0 + a1;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
+      if (sub == 0 && ok) {
         out_ids[j] = id;
-        out_lg[j] = a1 + bias[id];
-        if (j2 < hi) {
-          out_ids[j2] = id2;
-          out_lg[j2] = a2 + bias[id2];
-        }
+        out_lg[j] = a + bias[id];
       }
     }
   } else {
