@@ -82,7 +82,7 @@ def time_leaf_conv(sp, reps: int = 5):
     """The dominant kernel of the self-play step, timed live with HIP events on the stream it is
     launched on: `reps` eager forwards of the leaf net on the search's last leaf batch (the
     graph-captured forward is the same kernel sequence), one event pair around each launch of
-    k_tower_wino (the fused residual tower, bk_resnet_tower) or, when the tower runs per layer
+    k_tower_wino (the fused residual tower + heads, bk_resnet_tower_heads) or, when the tower runs per layer
     (BK_TOWER=0 or an unsupported board size), around each residual-block k_conv3x3 launch.
     -> dict(ms per launch, FLOP per launch, kernel name, direct-conv FLOP per launch, launches per
     leaf batch) or None (no HIP ResNet). FLOP = the arithmetic the kernel's MFMAs execute: for the
@@ -100,7 +100,7 @@ def time_leaf_conv(sp, reps: int = 5):
     obs = sp.evaluator.static_obs
     st = torch.cuda.current_stream(sp.eng.device)
     events = []
-    orig_conv, orig_tower = nets.conv3x3, nets.resnet_tower
+    orig_conv, orig_tower, orig_th = nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads
 
     def timed(fn):
         def run(*a, **k):
@@ -110,18 +110,18 @@ def time_leaf_conv(sp, reps: int = 5):
             e0.record(st)
             y = fn(*a, **k)
             e1.record(st)
-            events.append((e0, e1, fn is orig_tower))
+            events.append((e0, e1, fn is not orig_conv))
             return y
         return run
 
-    nets.conv3x3, nets.resnet_tower = timed(orig_conv), timed(orig_tower)
+    nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads = timed(orig_conv), timed(orig_tower), timed(orig_th)
     try:
         model(obs)  # warm
         events.clear()
         for _ in range(reps):
             model(obs)
     finally:
-        nets.conv3x3, nets.resnet_tower = orig_conv, orig_tower
+        nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads = orig_conv, orig_tower, orig_th
     torch.cuda.synchronize()
     if not events:
         return None
@@ -131,8 +131,9 @@ def time_leaf_conv(sp, reps: int = 5):
     direct = 2.0 * G * N * N * 64 * 9 * 64 * layers
     if load_library().bk_conv3x3_form(N, 64) == 1:
         flop = 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2 * layers
-        name = ("k_tower_wino (the fused residual tower: %d Winograd F(2x2,3x3) f32 MFMA convs 64->64, "
-                "bias/ReLU/residual fused, one workgroup per board)" % nconv if fused else
+        name = ("k_tower_wino (the fused residual tower + heads: %d Winograd F(2x2,3x3) f32 MFMA convs 64->64, "
+                "bias/ReLU/residual fused, the heads' 1x1 convs and value MLP after them, one workgroup per board)"
+                % nconv if fused else
                 "k_conv3x3_wino2 (Winograd F(2x2,3x3), f32 MFMA, 64->64, fused bias+ReLU)")
     else:
         flop, name = direct, "k_conv3x3 (direct, f32 MFMA, 64->64, fused bias+ReLU)"

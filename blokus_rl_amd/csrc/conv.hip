@@ -635,10 +635,20 @@ struct W2Lane {
 
 // the fused tower's epilogue: ReLU as data (max with floor: 0, or -inf for none), the residual
 // (RES, the tower's last conv) from res
-template <bool RES>
+// The ResNet heads' 1x1 convs (blokus_nnet.py:146-150), fused into the tower's last layer: per
+// output pixel, the dot products of its 64 channels with the 2 policy and 1 value filters. A lane
+// holds 4 channels of 4 pixels; the 4 lanes of a tile (l >> 4) meet in two xor-shuffles, and
+// each wave's 16-channel partials go to hp[pixel][wave][3] in LDS (summed in a fixed order later).
+struct HeadLane {
+  f32x4 wp0, wp1, wv;  // the lane's 4 channels of the three 1x1 filters
+  float* hp;           // LDS [NN][4][3]
+};
+
+template <bool RES, bool HEADS = false>
 __device__ __forceinline__ void w2_epilogue_flags(const W2Lane& c, const f32x4 (&acc)[16], int opix, int N,
                                                   float floor, __amdgpu_buffer_rsrc_t res,
-                                                  __amdgpu_buffer_rsrc_t y) {
+                                                  __amdgpu_buffer_rsrc_t y, bool store = true,
+                                                  const HeadLane* hl = nullptr) {
   if (opix < 0) return;
   f32x2 yv[4][2];
 #pragma unroll
@@ -666,8 +676,26 @@ __device__ __forceinline__ void w2_epilogue_flags(const W2Lane& c, const f32x4 (
       hi = pk_add(hi, rr.zw);
     }
     const f32x4 out = f32x4{fmaxf(lo.x, floor), fmaxf(lo.y, floor), fmaxf(hi.x, floor), fmaxf(hi.y, floor)};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out), y, o,
-                                           0, 0);
+    if (store)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out), y,
+                                             o, 0, 0);
+    if (HEADS) {
+      float d[3];
+      const f32x4* w[3] = {&hl->wp0, &hl->wp1, &hl->wv};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float a = out.x * (*w[k]).x + out.y * (*w[k]).y + out.z * (*w[k]).z + out.w * (*w[k]).w;
+        a += __shfl_xor(a, 16);
+        a += __shfl_xor(a, 32);
+        d[k] = a;
+      }
+      if ((c.l >> 4) == 0) {
+        float* dst = hl->hp + ((opix + (px >> 1) * N + (px & 1)) * 4 + c.wave) * 3;
+        dst[0] = d[0];
+        dst[1] = d[1];
+        dst[2] = d[2];
+      }
+    }
   }
 }
 
@@ -905,9 +933,9 @@ struct Tower {
 
 // One (layer, group) pair of the tower pipeline, MODE kW2First / kW2Mid / kW2Last (a layer's last
 // group: the next pair is (layer + 1, 0) and U is refilled with the next layer's)
-template <int M, bool WINDOW_IN_RAW, int N>
+template <int M, bool WINDOW_IN_RAW, bool HEADS, int N>
 __device__ __forceinline__ void tower_pair(const Tower<N>& t, f32x4 (&ur)[64], f32x4 (&raw)[16], f32x4& bias4,
-                                           int layer, int grp) {
+                                           int layer, int grp, const HeadLane& hl, bool store_last) {
   const bool last = layer + 1 == t.nlayers, relu = last || !(layer & 1);
   // the next pair: (layer, grp + 1), or (layer + 1, 0) after a layer's last group (the last pair of
   // the tower re-reads its own window into the idle V buffer: unconditional work)
@@ -921,8 +949,9 @@ __device__ __forceinline__ void tower_pair(const Tower<N>& t, f32x4 (&ur)[64], f
   const int l = t.c.l, wave = t.c.wave;
   if (layer == 2) W2STAMP(10 + grp, __builtin_amdgcn_s_memtime());
 #endif
-  if (last)  // the tower's last conv: + the tower input (a uniform branch)
-    w2_epilogue_flags<true>(t.c, acc, t.out_pixel(grp), N, 0.0f, t.res_of(layer), t.out_of(layer));
+  if (last)  // the tower's last conv: + the tower input (a uniform branch), and the heads' 1x1 convs
+    w2_epilogue_flags<true, HEADS>(t.c, acc, t.out_pixel(grp), N, 0.0f, t.res_of(layer), t.out_of(layer), store_last,
+                                   &hl);
   else
     w2_epilogue_flags<false>(t.c, acc, t.out_pixel(grp), N, relu ? 0.0f : -__builtin_inff(), t.res_of(layer),
                              t.out_of(layer));
@@ -936,11 +965,22 @@ __device__ __forceinline__ void tower_pair(const Tower<N>& t, f32x4 (&ur)[64], f
 #endif
 }
 
-template <int N>
+// The heads after the tower (k_tower_wino<N, true>): the 1x1 convs' weights, the value MLP, the
+// outputs (policy features pf [B][2*NN] channel-major, values v [B][P]); out may be skipped.
+struct TowerHeads {
+  const float *wp, *bp, *wv, *bv, *w1t, *b1, *w2, *b2;
+  int P;
+  float* pf;
+  float* v;
+  int store_out;
+};
+
+template <int N, bool HEADS>
 __global__ __launch_bounds__(kW2Threads, 1) void k_tower_wino(const float* __restrict__ x0, float* hA, float* hB,
                                                               float* __restrict__ out,
                                                               const float* __restrict__ u2all,
-                                                              const float* __restrict__ biasall, int nlayers) {
+                                                              const float* __restrict__ biasall, int nlayers,
+                                                              TowerHeads hd) {
   extern __shared__ __attribute__((aligned(16))) float v_lds[];  // [2 buf][16 s][16 p][16 t][4 g]
   static_assert(tower_pipeline_ok<N>(), "k_tower_wino: board too small for the cross-layer pipeline");
   constexpr int NG = Tower<N>::NG;
@@ -985,14 +1025,65 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_tower_wino(const float* __res
   }
   __syncthreads();
   W2STAMP(1, __builtin_amdgcn_s_memtime());
-  tower_pair<kW2First, true>(t, ur, raw, bias4, 0, 0);
-  for (int grp = 1; grp < NG - 1; ++grp) tower_pair<kW2Mid, false>(t, ur, raw, bias4, 0, grp);
-  tower_pair<kW2Last, false>(t, ur, raw, bias4, 0, NG - 1);
+  HeadLane hl;
+  constexpr int NN = N * N;
+  if (HEADS) {
+    const int ch = 16 * wave + 4 * (l >> 4);
+    hl.wp0 = *reinterpret_cast<const f32x4*>(hd.wp + ch);
+    hl.wp1 = *reinterpret_cast<const f32x4*>(hd.wp + 64 + ch);
+    hl.wv = *reinterpret_cast<const f32x4*>(hd.wv + ch);
+    hl.hp = v_lds + 2 * kW2VBuf;
+  }
+  const bool so = !HEADS || hd.store_out;
+  tower_pair<kW2First, true, HEADS>(t, ur, raw, bias4, 0, 0, hl, so);
+  for (int grp = 1; grp < NG - 1; ++grp) tower_pair<kW2Mid, false, HEADS>(t, ur, raw, bias4, 0, grp, hl, so);
+  tower_pair<kW2Last, false, HEADS>(t, ur, raw, bias4, 0, NG - 1, hl, so);
   for (int layer = 1; layer < nlayers; ++layer) {
-    tower_pair<kW2First, false>(t, ur, raw, bias4, layer, 0);
-    for (int grp = 1; grp < NG - 1; ++grp) tower_pair<kW2Mid, false>(t, ur, raw, bias4, layer, grp);
-    tower_pair<kW2Last, false>(t, ur, raw, bias4, layer, NG - 1);
+    tower_pair<kW2First, false, HEADS>(t, ur, raw, bias4, layer, 0, hl, so);
+    for (int grp = 1; grp < NG - 1; ++grp) tower_pair<kW2Mid, false, HEADS>(t, ur, raw, bias4, layer, grp, hl, so);
+    tower_pair<kW2Last, false, HEADS>(t, ur, raw, bias4, layer, NG - 1, hl, so);
     if (layer == 2) W2STAMP(2, __builtin_amdgcn_s_memtime());
+  }
+  if (HEADS) {
+    // the heads (blokus_nnet.py:146-150, BN folded), as k_resnet_heads but from the partials in hp:
+    // pf = relu(1x1 conv + bp) (channel-major), vfeat = relu(value 1x1 conv + bv) in LDS, then
+    // v = tanh(W2 relu(W1 vfeat + b1) + b2); the 4 waves sweep quarters of W1's inputs
+    const float* hp = hl.hp;
+    float* vfeat = v_lds;  // the V buffers are free now
+    float* part = v_lds + NN;
+    const int bi = blockIdx.x, tid = threadIdx.x;
+    for (int i = tid; i < NN; i += kW2Threads) {
+      const float* q = hp + i * 12;
+      const float p0 = ((q[0] + q[3]) + q[6]) + q[9], p1 = ((q[1] + q[4]) + q[7]) + q[10],
+                  pv = ((q[2] + q[5]) + q[8]) + q[11];
+      hd.pf[(size_t)bi * 2 * NN + i] = fmaxf(p0 + hd.bp[0], 0.0f);
+      hd.pf[(size_t)bi * 2 * NN + NN + i] = fmaxf(p1 + hd.bp[1], 0.0f);
+      vfeat[i] = fmaxf(pv + hd.bv[0], 0.0f);
+    }
+    __syncthreads();
+    const int q0 = (NN * wave) / 4, q1 = (NN * (wave + 1)) / 4;
+    float acc0 = 0.f, acc1 = 0.f;
+    int i = q0;
+    for (; i + 10 <= q1; i += 10) {
+      float w[10];
+#pragma unroll
+      for (int u = 0; u < 10; ++u) w[u] = hd.w1t[(size_t)(i + u) * 64 + l];
+#pragma unroll
+      for (int u = 0; u < 10; u += 2) {
+        acc0 += w[u] * vfeat[i + u];
+        acc1 += w[u + 1] * vfeat[i + u + 1];
+      }
+    }
+    for (; i < q1; ++i) acc0 += hd.w1t[(size_t)i * 64 + l] * vfeat[i];
+    part[wave * 64 + l] = acc0 + acc1;
+    __syncthreads();
+    if (wave == 0) {
+      const float h = fmaxf(((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) + hd.b1[l], 0.0f);
+      for (int q = 0; q < hd.P; ++q) {
+        const float sum = wave_sum_f(hd.w2[q * 64 + l] * h);
+        if (l == 0) hd.v[(size_t)bi * hd.P + q] = tanhf(sum + hd.b2[q]);
+      }
+    }
   }
   W2STAMP(29, __builtin_amdgcn_s_memtime());
   W2STAMP(31, __builtin_amdgcn_s_memrealtime());
@@ -1037,31 +1128,62 @@ int bk_conv3x3_packed_floats(int cin) {
 int bk_tower_u_floats(void) { return kW2UFloats; }
 int bk_tower_supported(int N) { return N == 14 || N == 20; }
 
-int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
-                    float* hB, float* out, void* stream) {
-  BK_REQUIRE(x0 && u2all && biasall && hA && hB && out && B >= 0 && nlayers >= 1, "bad argument");
+namespace {
+int tower_launch(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
+                 float* hB, float* out, const TowerHeads* hd, void* stream) {
+  BK_REQUIRE(x0 && u2all && biasall && hA && hB && B >= 0 && nlayers >= 1, "bad argument");
+  BK_REQUIRE(out || (hd && !hd->store_out), "bad argument");
   BK_REQUIRE(bk_tower_supported(N), "bk_resnet_tower: N must be 14 or 20");
   BK_REQUIRE(((uintptr_t)x0 & 15u) == 0 && ((uintptr_t)hA & 15u) == 0 && ((uintptr_t)hB & 15u) == 0 &&
                  ((uintptr_t)out & 15u) == 0 && ((uintptr_t)u2all & 15u) == 0 && ((uintptr_t)biasall & 15u) == 0,
              "bk_resnet_tower: 16-byte aligned buffers");
   BK_REQUIRE((int64_t)N * N * 256 < (1ll << 31), "bk_resnet_tower: board too large");
   if (B == 0) return BK_OK;
-  const int lds = (int)(sizeof(float) * 2 * kW2VBuf);
+  // V buffers (128 KB), then the heads' per-pixel partials [NN][4 waves][3]
+  const int lds = (int)(sizeof(float) * (2 * kW2VBuf + (hd ? N * N * 12 : 0)));
   static bool attr = false;
   if (!attr) {
-    const void* fns[2] = {(const void*)k_tower_wino<14>, (const void*)k_tower_wino<20>};
+    const void* fns[4] = {(const void*)k_tower_wino<14, false>, (const void*)k_tower_wino<20, false>,
+                          (const void*)k_tower_wino<14, true>, (const void*)k_tower_wino<20, true>};
     for (const void* fn : fns)
-      if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds), "hipFuncSetAttribute") !=
-          BK_OK)
+      if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(sizeof(float) * (2 * kW2VBuf + 20 * 20 * 12))),
+                    "hipFuncSetAttribute") != BK_OK)
         return BK_EHIP;
     attr = true;
   }
   hipStream_t s = (hipStream_t)stream;
-  if (N == 20)
-    hipLaunchKernelGGL(k_tower_wino<20>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
+  const TowerHeads h = hd ? *hd : TowerHeads{};
+  if (N == 20 && hd)
+    hipLaunchKernelGGL((k_tower_wino<20, true>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall,
+                       nlayers, h);
+  else if (N == 20)
+    hipLaunchKernelGGL((k_tower_wino<20, false>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall,
+                       nlayers, h);
+  else if (hd)
+    hipLaunchKernelGGL((k_tower_wino<14, true>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall,
+                       nlayers, h);
   else
-    hipLaunchKernelGGL(k_tower_wino<14>, dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall, nlayers);
+    hipLaunchKernelGGL((k_tower_wino<14, false>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall,
+                       nlayers, h);
   return launch_check("k_tower_wino");
+}
+}  // namespace
+
+int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
+                    float* hB, float* out, void* stream) {
+  BK_REQUIRE(out, "bad argument");
+  return tower_launch(x0, B, N, nlayers, u2all, biasall, hA, hB, out, nullptr, stream);
+}
+
+int bk_resnet_tower_heads(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall,
+                          float* hA, float* hB, float* out, const float* wp, const float* bp, const float* wv,
+                          const float* bv, const float* w1t, const float* b1, const float* w2, const float* b2, int P,
+                          float* pf, float* vout, void* stream) {
+  BK_REQUIRE(wp && bp && wv && bv && w1t && b1 && w2 && b2 && pf && vout && P > 0, "bad argument");
+  BK_REQUIRE(((uintptr_t)wp & 15u) == 0 && ((uintptr_t)wv & 15u) == 0, "bk_resnet_tower_heads: 16-byte aligned wp, wv");
+  TowerHeads h{wp, bp, wv, bv, w1t, b1, w2, b2, P, pf, vout, out ? 1 : 0};
+  return tower_launch(x0, B, N, nlayers, u2all, biasall, hA, hB, out, &h, stream);
 }
 
 int bk_conv3x3_form(int N, int cin) { return cin == 64 && N % 2 == 0 && !direct_only() ? 1 : 0; }

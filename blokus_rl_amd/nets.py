@@ -278,6 +278,33 @@ def resnet_tower(x: torch.Tensor, u2all: torch.Tensor, biasall: torch.Tensor, nl
     return out
 
 
+def resnet_tower_heads(x: torch.Tensor, u2all: torch.Tensor, biasall: torch.Tensor, nlayers: int, f: "FusedResNet",
+                       want_out: bool = False):
+    """bk_resnet_tower_heads: the tower and the heads in one launch, from the stem output x
+    [B, 64, N, N] channels_last -> (policy features [B, 2*N*N], values [B, P][, tower output])."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, C, N, _ = x.shape
+    assert C == 64 and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+    lib = load_library()
+    assert u2all.numel() == nlayers * lib.bk_tower_u_floats() and biasall.numel() == nlayers * 64
+    P = f.value_fc2.out_features
+    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=x.device)
+    v = torch.empty((B, P), dtype=torch.float32, device=x.device)
+    out = torch.empty_like(x, memory_format=torch.channels_last) if want_out else None
+    ha = torch.empty_like(x, memory_format=torch.channels_last)
+    hb = torch.empty_like(x, memory_format=torch.channels_last)
+    c = lambda t: t.detach().float().contiguous()  # noqa: E731
+    wp, wv = c(f.policy_conv.weight.view(2, 64)), c(f.value_conv.weight.view(64))
+    _check(lib.bk_resnet_tower_heads(ctypes.c_void_p(x.data_ptr()), B, N, nlayers, _ptr(u2all), _ptr(biasall),
+                                     ctypes.c_void_p(ha.data_ptr()), ctypes.c_void_p(hb.data_ptr()),
+                                     None if out is None else ctypes.c_void_p(out.data_ptr()), _ptr(wp),
+                                     _ptr(c(f.policy_conv.bias)), _ptr(wv), _ptr(c(f.value_conv.bias)),
+                                     _ptr(f.value_fc1_wt()), _ptr(c(f.value_fc1.bias)), _ptr(c(f.value_fc2.weight)),
+                                     _ptr(c(f.value_fc2.bias)), P, _ptr(pf), _ptr(v), _stream(x.device)))
+    return (pf, v, out) if want_out else (pf, v)
+
+
 def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
     """bk_resnet_heads: tower output [B, 64, N, N] channels_last -> (policy features [B, 2*N*N] in
     the NCHW flatten order, values [B, P])."""
@@ -335,14 +362,15 @@ class LeafResNet(nn.Module):
             from .engine import load_library
 
             if n and tower_enabled() and load_library().bk_tower_supported(x.shape[2]):
-                h = resnet_tower(x, self.u_tower, self.b_tower, 2 * n)
+                # the tower and the heads in one launch (bk_resnet_tower_heads)
+                pf, v = resnet_tower_heads(x, self.u_tower, self.b_tower, 2 * n, f)
             else:
                 for i, (c1, c2) in enumerate(f.blocks):
                     h = conv3x3(h, getattr(self, f"w_{i}_1"), c1.bias, True)
                     h = conv3x3(h, getattr(self, f"w_{i}_2"), c2.bias, i + 1 == n, x if i + 1 == n else None)
-            if not n:
-                h = torch.relu(x + x)
-            pf, v = resnet_heads(h, f)
+                if not n:
+                    h = torch.relu(x + x)
+                pf, v = resnet_heads(h, f)
             if self.features:
                 return pf, v
             logits = f.policy_out(pf)

@@ -270,6 +270,13 @@ int bk_tower_u_floats(void);
 int bk_tower_supported(int N);
 int bk_resnet_tower(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall, float* hA,
                     float* hB, float* out, void* stream);
+/* The tower followed by the heads in the same launch (blokus_nnet.py:140-150): the last conv's
+ * epilogue takes the 1x1 convs, then the value MLP runs per board; pf, vout, and the head weights
+ * as bk_resnet_heads. out may be NULL (the tower output is then not written). */
+int bk_resnet_tower_heads(const float* x0, int B, int N, int nlayers, const float* u2all, const float* biasall,
+                          float* hA, float* hB, float* out, const float* wp, const float* bp, const float* wv,
+                          const float* bv, const float* w1t, const float* b1, const float* w2, const float* b2, int P,
+                          float* pf, float* vout, void* stream);
 
 #ifdef __cplusplus
 }

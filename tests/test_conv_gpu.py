@@ -156,3 +156,33 @@ def test_resnet_tower_matches_per_layer_convs(B, N, nblocks):
             ref = torch.relu(ref)
     ref = torch.relu(ref + x.double())
     assert float((out.double() - ref).abs().max()) <= 1e-4 * (float(ref.abs().max()) + 1.0)
+
+
+@pytest.mark.parametrize("B,N,nblocks", [(256, 20, 5), (3, 20, 2), (37, 14, 2)])
+def test_resnet_tower_heads_matches_tower_then_heads(B, N, nblocks):
+    """bk_resnet_tower_heads (heads fused into the tower launch): the tower output bitwise equal
+    to bk_resnet_tower, policy features and values equal to bk_resnet_heads on it to f32
+    rounding (the 1x1 convs sum the 64 channels in a different order)."""
+    from blokus_rl_amd.nets import FusedResNet, ResNet, pack_tower, resnet_heads, resnet_tower, resnet_tower_heads
+
+    torch.manual_seed(B + N)
+    net = ResNet(N, 4, 100, nblocks).cuda().eval()
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    f = FusedResNet(net).eval()
+    convs = [c for blk in f.blocks for c in blk]
+    ut = pack_tower([c.weight.detach() for c in convs])
+    bt = torch.cat([c.bias.detach().float() for c in convs]).contiguous()
+    x = torch.relu(torch.randn((B, 64, N, N), device="cuda")).contiguous(memory_format=torch.channels_last)
+    h = resnet_tower(x, ut, bt, 2 * nblocks)
+    pf_ref, v_ref = resnet_heads(h, f)
+    pf, v, out = resnet_tower_heads(x, ut, bt, 2 * nblocks, f, want_out=True)
+    pf2, v2 = resnet_tower_heads(x, ut, bt, 2 * nblocks, f)
+    torch.cuda.synchronize()
+    assert torch.equal(out, h)
+    assert torch.equal(pf, pf2) and torch.equal(v, v2)
+    assert torch.allclose(pf, pf_ref, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(v, v_ref, rtol=1e-5, atol=1e-6)
