@@ -101,6 +101,7 @@ def time_leaf_conv(sp, reps: int = 5):
     st = torch.cuda.current_stream(sp.eng.device)
     events = []
     orig_conv, orig_tower, orig_th = nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads
+    orig_sth = nets.resnet_stem_tower_heads
 
     def timed(fn):
         def run(*a, **k):
@@ -110,11 +111,12 @@ def time_leaf_conv(sp, reps: int = 5):
             e0.record(st)
             y = fn(*a, **k)
             e1.record(st)
-            events.append((e0, e1, fn is not orig_conv))
+            events.append((e0, e1, fn is not orig_conv, fn is orig_sth))
             return y
         return run
 
     nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads = timed(orig_conv), timed(orig_tower), timed(orig_th)
+    nets.resnet_stem_tower_heads = timed(orig_sth)
     try:
         model(obs)  # warm
         events.clear()
@@ -122,18 +124,20 @@ def time_leaf_conv(sp, reps: int = 5):
             model(obs)
     finally:
         nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads = orig_conv, orig_tower, orig_th
+        nets.resnet_stem_tower_heads = orig_sth
     torch.cuda.synchronize()
     if not events:
         return None
-    fused = events[0][2]
-    ms = sum(a.elapsed_time(b) for a, b, _ in events) / len(events)
+    fused, with_stem = events[0][2], events[0][3]
+    ms = sum(ev[0].elapsed_time(ev[1]) for ev in events) / len(events)
     layers = nconv if fused else 1
-    direct = 2.0 * G * N * N * 64 * 9 * 64 * layers
+    stem = 2.0 * G * N * N * 64 * 9 * model.f.stem.in_channels if with_stem else 0.0
+    direct = 2.0 * G * N * N * 64 * 9 * 64 * layers + stem
     if load_library().bk_conv3x3_form(N, 64) == 1:
-        flop = 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2 * layers
-        name = ("k_tower_wino (the fused residual tower + heads: %d Winograd F(2x2,3x3) f32 MFMA convs 64->64, "
-                "bias/ReLU/residual fused, the heads' 1x1 convs and value MLP after them, one workgroup per board)"
-                % nconv if fused else
+        flop = 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2 * layers + stem
+        name = ("k_tower_wino (the leaf ResNet in one launch, one workgroup per board: %sthe residual tower of "
+                "%d Winograd F(2x2,3x3) f32 MFMA convs 64->64 with bias/ReLU/residual fused, the heads' 1x1 convs and "
+                "value MLP)" % ("the stem conv (direct, f32 MFMA), " if with_stem else "", nconv) if fused else
                 "k_conv3x3_wino2 (Winograd F(2x2,3x3), f32 MFMA, 64->64, fused bias+ReLU)")
     else:
         flop, name = direct, "k_conv3x3 (direct, f32 MFMA, 64->64, fused bias+ReLU)"

@@ -965,6 +965,50 @@ __device__ __forceinline__ void tower_pair(const Tower<N>& t, f32x4 (&ur)[64], f
 #endif
 }
 
+// The stem conv (blokus_nnet.py:137, BN folded: conv3x3 8 -> 64 channels + bias + ReLU) of one
+// board inside the tower launch: the planar observation staged zero-padded in LDS, then per wave
+// (16 output channels) NN/16 pixel tiles x 18 k-steps of v_mfma_f32_16x16x4_f32 with A = im2col
+// entries read from LDS at immediate offsets (k-step s = tap s/2, channels 4(s%2)..+3) and B =
+// the packed weights in 18 registers (nets.pack_stem_tower); bias + ReLU into x0 (NHWC).
+constexpr int kStemCin = 8;
+template <int N>
+__device__ __forceinline__ void tower_stem(float* lds, const float* __restrict__ obs_b, const float* __restrict__ wst,
+                                           const float* __restrict__ bst, __amdgpu_buffer_rsrc_t x0r, int wave, int l) {
+  constexpr int NP = N + 2, NN = N * N, TILES = (NN + 15) / 16;
+  for (int i = threadIdx.x; i < kStemCin * NP * NP; i += kW2Threads) {
+    const int ch = i / (NP * NP), r = i - ch * NP * NP, y = r / NP - 1, x = r - (r / NP) * NP - 1;
+    lds[i] = (y >= 0 && y < N && x >= 0 && x < N) ? obs_b[ch * NN + y * N + x] : 0.0f;
+  }
+  float wb[18];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) wb[s] = wst[(wave * 18 + s) * kWave + l];
+  const int g = l >> 4, m = l & 15;
+  const float bm = bst[16 * wave + m];
+  __syncthreads();
+  for (int tile = 0; tile < TILES; ++tile) {
+    const int p = tile * 16 + m, pc = p < NN ? p : NN - 1, py = pc / N, px = pc - (pc / N) * N;
+    const float* a = lds + g * NP * NP + py * NP + px;  // channel g, window top-left (padded)
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int t = s >> 1;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * (s & 1) * NP * NP + (t / 3) * NP + (t % 3)], wb[s], acc, 0, 0, 0);
+    }
+    // D: lane (g, m) holds pixels tile*16 + 4g + r, output channel 16 wave + m
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pix = tile * 16 + 4 * g + r;
+      if (pix < NN)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, fmaxf(acc[r] + bm, 0.0f)), x0r,
+                                              (unsigned)(pix * 64 + 16 * wave + m) * 4, 0, 0);
+    }
+  }
+  // x0 complete and visible to the workgroup before the tower reads its windows
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");
+}
+
 // The heads after the tower (k_tower_wino<N, true>): the 1x1 convs' weights, the value MLP, the
 // outputs (policy features pf [B][2*NN] channel-major, values v [B][P]); out may be skipped.
 struct TowerHeads {
@@ -973,9 +1017,12 @@ struct TowerHeads {
   float* pf;
   float* v;
   int store_out;
+  const float* obs;  // non-null: the stem runs first (k_tower_wino<N, true, true>) and x0 is its output
+  const float* wstem;
+  const float* bstem;
 };
 
-template <int N, bool HEADS>
+template <int N, bool HEADS, bool STEM = false>
 __global__ __launch_bounds__(kW2Threads, 1) void k_tower_wino(const float* __restrict__ x0, float* hA, float* hB,
                                                               float* __restrict__ out,
                                                               const float* __restrict__ u2all,
@@ -1004,6 +1051,7 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_tower_wino(const float* __res
   t.biasall = biasall;
   t.nlayers = nlayers;
   t.c.xr = t.in_of(0);
+  if (STEM) tower_stem<N>(v_lds, hd.obs + (size_t)blockIdx.x * kStemCin * N * N, hd.wstem, hd.bstem, t.c.xr, wave, l);
   // prologue: windows of pairs (0, 0) and (0, 1), layer 0's bias and U of k-steps 0, 1
   f32x4 ur[64];
   f32x4 raw[16];
@@ -1143,8 +1191,9 @@ int tower_launch(const float* x0, int B, int N, int nlayers, const float* u2all,
   const int lds = (int)(sizeof(float) * (2 * kW2VBuf + (hd ? N * N * 12 : 0)));
   static bool attr = false;
   if (!attr) {
-    const void* fns[4] = {(const void*)k_tower_wino<14, false>, (const void*)k_tower_wino<20, false>,
-                          (const void*)k_tower_wino<14, true>, (const void*)k_tower_wino<20, true>};
+    const void* fns[6] = {(const void*)k_tower_wino<14, false>, (const void*)k_tower_wino<20, false>,
+                          (const void*)k_tower_wino<14, true>,  (const void*)k_tower_wino<20, true>,
+                          (const void*)k_tower_wino<14, true, true>, (const void*)k_tower_wino<20, true, true>};
     for (const void* fn : fns)
       if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)(sizeof(float) * (2 * kW2VBuf + 20 * 20 * 12))),
@@ -1154,7 +1203,13 @@ int tower_launch(const float* x0, int B, int N, int nlayers, const float* u2all,
   }
   hipStream_t s = (hipStream_t)stream;
   const TowerHeads h = hd ? *hd : TowerHeads{};
-  if (N == 20 && hd)
+  if (N == 20 && hd && hd->obs)
+    hipLaunchKernelGGL((k_tower_wino<20, true, true>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all,
+                       biasall, nlayers, h);
+  else if (N == 14 && hd && hd->obs)
+    hipLaunchKernelGGL((k_tower_wino<14, true, true>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all,
+                       biasall, nlayers, h);
+  else if (N == 20 && hd)
     hipLaunchKernelGGL((k_tower_wino<20, true>), dim3(B), dim3(kW2Threads), lds, s, x0, hA, hB, out, u2all, biasall,
                        nlayers, h);
   else if (N == 20)
@@ -1182,7 +1237,22 @@ int bk_resnet_tower_heads(const float* x0, int B, int N, int nlayers, const floa
                           float* pf, float* vout, void* stream) {
   BK_REQUIRE(wp && bp && wv && bv && w1t && b1 && w2 && b2 && pf && vout && P > 0, "bad argument");
   BK_REQUIRE(((uintptr_t)wp & 15u) == 0 && ((uintptr_t)wv & 15u) == 0, "bk_resnet_tower_heads: 16-byte aligned wp, wv");
-  TowerHeads h{wp, bp, wv, bv, w1t, b1, w2, b2, P, pf, vout, out ? 1 : 0};
+  TowerHeads h{wp, bp, wv, bv, w1t, b1, w2, b2, P, pf, vout, out ? 1 : 0, nullptr, nullptr, nullptr};
+  return tower_launch(x0, B, N, nlayers, u2all, biasall, hA, hB, out, &h, stream);
+}
+
+int bk_stem_tower_u_floats(void) { return 4 * 18 * kWave; }
+
+int bk_resnet_stem_tower_heads(const float* obs, int B, int N, int cin, const float* wstem, const float* bstem,
+                               int nlayers, const float* u2all, const float* biasall, float* x0, float* hA, float* hB,
+                               float* out, const float* wp, const float* bp, const float* wv, const float* bv,
+                               const float* w1t, const float* b1, const float* w2, const float* b2, int P, float* pf,
+                               float* vout, void* stream) {
+  BK_REQUIRE(obs && wstem && bstem && x0, "bad argument");
+  BK_REQUIRE(cin == kStemCin, "bk_resnet_stem_tower_heads: the stem takes 8 observation planes");
+  BK_REQUIRE(wp && bp && wv && bv && w1t && b1 && w2 && b2 && pf && vout && P > 0, "bad argument");
+  BK_REQUIRE(((uintptr_t)wp & 15u) == 0 && ((uintptr_t)wv & 15u) == 0, "bk_resnet_stem_tower_heads: 16-byte aligned wp, wv");
+  TowerHeads h{wp, bp, wv, bv, w1t, b1, w2, b2, P, pf, vout, out ? 1 : 0, obs, wstem, bstem};
   return tower_launch(x0, B, N, nlayers, u2all, biasall, hA, hB, out, &h, stream);
 }
 

@@ -70,6 +70,9 @@ _SIGS = {
     "bk_resnet_tower": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bk_resnet_tower_heads": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _i, _vp, _vp, _vp]),
+    "bk_stem_tower_u_floats": (_i, []),
+    "bk_resnet_stem_tower_heads": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                        _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
 }
 
 _LIB = None

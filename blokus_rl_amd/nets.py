@@ -253,6 +253,19 @@ def pack_tower(weights) -> torch.Tensor:
     return torch.cat([pack_winograd(w)[-(4 * 64 * 64 * 4):] for w in weights]).contiguous()
 
 
+def pack_stem_tower(w: torch.Tensor) -> torch.Tensor:
+    """[64, 8, 3, 3] stem weights -> bk_resnet_stem_tower_heads' MFMA order: flat [4 blocks kb]
+    [18 k-steps s][64 lanes], element = w[16kb + (l & 15), 4 * (s % 2) + (l >> 4), t // 3, t % 3]
+    with tap t = s // 2."""
+    assert w.shape == (64, 8, 3, 3)
+    dev = w.device
+    kb = torch.arange(4, device=dev).view(4, 1, 1)
+    st = torch.arange(18, device=dev).view(1, 18, 1)
+    lane = torch.arange(64, device=dev).view(1, 1, 64)
+    t = st // 2
+    return w.float()[16 * kb + (lane & 15), 4 * (st % 2) + (lane >> 4), t // 3, t % 3].contiguous().view(-1)
+
+
 def tower_enabled() -> bool:
     """BK_TOWER=0 runs the residual tower as one bk_conv3x3 launch per layer instead of the fused
     bk_resnet_tower (same arithmetic; for comparisons)."""
@@ -305,6 +318,33 @@ def resnet_tower_heads(x: torch.Tensor, u2all: torch.Tensor, biasall: torch.Tens
     return (pf, v, out) if want_out else (pf, v)
 
 
+def resnet_stem_tower_heads(obs: torch.Tensor, wstem: torch.Tensor, u2all: torch.Tensor, biasall: torch.Tensor,
+                            nlayers: int, f: "FusedResNet", want_x0: bool = False):
+    """bk_resnet_stem_tower_heads: the planar observation [B, 8, N, N] -> (policy features
+    [B, 2*N*N], values [B, P][, the stem output x0]) in one launch: stem conv, tower, heads."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, cin, N, _ = obs.shape
+    assert cin == 8 and obs.dtype == torch.float32 and obs.is_contiguous()
+    lib = load_library()
+    assert wstem.numel() == lib.bk_stem_tower_u_floats()
+    assert u2all.numel() == nlayers * lib.bk_tower_u_floats() and biasall.numel() == nlayers * 64
+    P = f.value_fc2.out_features
+    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=obs.device)
+    v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
+    x0 = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device, memory_format=torch.channels_last)
+    ha, hb = torch.empty_like(x0), torch.empty_like(x0)
+    c = lambda t: t.detach().float().contiguous()  # noqa: E731
+    wp, wv = c(f.policy_conv.weight.view(2, 64)), c(f.value_conv.weight.view(64))
+    _check(lib.bk_resnet_stem_tower_heads(
+        ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(wstem), _ptr(c(f.stem.bias)), nlayers, _ptr(u2all),
+        _ptr(biasall), ctypes.c_void_p(x0.data_ptr()), ctypes.c_void_p(ha.data_ptr()), ctypes.c_void_p(hb.data_ptr()),
+        None, _ptr(wp), _ptr(c(f.policy_conv.bias)), _ptr(wv), _ptr(c(f.value_conv.bias)), _ptr(f.value_fc1_wt()),
+        _ptr(c(f.value_fc1.bias)), _ptr(c(f.value_fc2.weight)), _ptr(c(f.value_fc2.bias)), P, _ptr(pf), _ptr(v),
+        _stream(obs.device)))
+    return (pf, v, x0) if want_x0 else (pf, v)
+
+
 def resnet_heads(x: torch.Tensor, f: "FusedResNet"):
     """bk_resnet_heads: tower output [B, 64, N, N] channels_last -> (policy features [B, 2*N*N] in
     the NCHW flatten order, values [B, P])."""
@@ -346,6 +386,8 @@ class LeafResNet(nn.Module):
             for i, (c1, c2) in enumerate(f.blocks):
                 self.register_buffer(f"w_{i}_1", pack_conv3x3(c1.weight.detach()))
                 self.register_buffer(f"w_{i}_2", pack_conv3x3(c2.weight.detach()))
+            if f.stem.in_channels == 8:  # the stem inside the tower launch (bk_resnet_stem_tower_heads)
+                self.register_buffer("w_stem_tower", pack_stem_tower(f.stem.weight.detach()))
             if len(f.blocks):  # the fused tower's operands (bk_resnet_tower)
                 convs = [c for blk in f.blocks for c in blk]
                 self.register_buffer("u_tower", pack_tower([c.weight.detach() for c in convs]))
@@ -357,11 +399,20 @@ class LeafResNet(nn.Module):
         n = len(f.blocks)
         if self.native:
             # planar observation in (as the search writes it), NHWC activations through the tower
-            x = conv3x3(x.float().contiguous(), self.w_stem, f.stem.bias, True)
-            h = x
             from .engine import load_library
 
-            if n and tower_enabled() and load_library().bk_tower_supported(x.shape[2]):
+            fused = n and tower_enabled() and load_library().bk_tower_supported(x.shape[2])
+            if fused and f.stem.in_channels == 8:
+                # stem conv, tower and heads in one launch (bk_resnet_stem_tower_heads)
+                pf, v = resnet_stem_tower_heads(x.float().contiguous(), self.w_stem_tower, self.u_tower, self.b_tower,
+                                                2 * n, f)
+                if self.features:
+                    return pf, v
+                logits = f.policy_out(pf)
+                return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
+            x = conv3x3(x.float().contiguous(), self.w_stem, f.stem.bias, True)
+            h = x
+            if fused:
                 # the tower and the heads in one launch (bk_resnet_tower_heads)
                 pf, v = resnet_tower_heads(x, self.u_tower, self.b_tower, 2 * n, f)
             else:

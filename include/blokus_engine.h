@@ -277,6 +277,16 @@ int bk_resnet_tower_heads(const float* x0, int B, int N, int nlayers, const floa
                           float* hA, float* hB, float* out, const float* wp, const float* bp, const float* wv,
                           const float* bv, const float* w1t, const float* b1, const float* w2, const float* b2, int P,
                           float* pf, float* vout, void* stream);
+/* The whole leaf ResNet body in one launch: the stem conv (8 observation planes -> 64, + bias,
+ * ReLU; blokus_nnet.py:137) from the planar observation obs [B][8][N][N] into x0 (written), then
+ * bk_resnet_tower_heads. wstem: bk_stem_tower_u_floats() floats in the kernel's MFMA order
+ * (nets.py pack_stem_tower), bstem [64]. */
+int bk_stem_tower_u_floats(void);
+int bk_resnet_stem_tower_heads(const float* obs, int B, int N, int cin, const float* wstem, const float* bstem,
+                               int nlayers, const float* u2all, const float* biasall, float* x0, float* hA, float* hB,
+                               float* out, const float* wp, const float* bp, const float* wv, const float* bv,
+                               const float* w1t, const float* b1, const float* w2, const float* b2, int P, float* pf,
+                               float* vout, void* stream);
 
 #ifdef __cplusplus
 }

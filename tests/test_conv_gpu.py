@@ -186,3 +186,45 @@ def test_resnet_tower_heads_matches_tower_then_heads(B, N, nblocks):
     assert torch.equal(pf, pf2) and torch.equal(v, v2)
     assert torch.allclose(pf, pf_ref, rtol=1e-5, atol=1e-5)
     assert torch.allclose(v, v_ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,N,nblocks", [(256, 20, 5), (3, 20, 2), (37, 14, 1)])
+def test_resnet_stem_tower_heads_matches_separate_launches(B, N, nblocks):
+    """bk_resnet_stem_tower_heads (stem conv + tower + heads in one launch) against the separate
+    stem bk_conv3x3 + bk_resnet_tower_heads: the stem output to f32 rounding (different K order),
+    and the heads' outputs within the f32 bound of the fp64 torch reference of the whole net."""
+    from blokus_rl_amd.nets import (FusedResNet, ResNet, pack_stem_tower, pack_tower, resnet_stem_tower_heads)
+
+    torch.manual_seed(B * 7 + N)
+    net = ResNet(N, 4, 100, nblocks).cuda().eval()
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    f = FusedResNet(net).eval()
+    convs = [c for blk in f.blocks for c in blk]
+    ut = pack_tower([c.weight.detach() for c in convs])
+    bt = torch.cat([c.bias.detach().float() for c in convs]).contiguous()
+    obs = (torch.rand((B, 8, N, N), device="cuda") < 0.3).float()
+    pf, v, x0 = resnet_stem_tower_heads(obs, pack_stem_tower(f.stem.weight.detach()), ut, bt, 2 * nblocks, f,
+                                        want_x0=True)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref_x0 = torch.relu(F.conv2d(obs.double(), f.stem.weight.double(), f.stem.bias.double(), padding=1))
+    assert float((x0.double() - ref_x0).abs().max()) <= 1e-5 * (float(ref_x0.abs().max()) + 1.0)
+    with torch.no_grad():
+        fd = FusedResNet(net).double().eval()
+        p_ref = torch.relu(fd.policy_conv(_tower_ref(fd, obs.double()))).flatten(1)
+        xt = _tower_ref(fd, obs.double())
+        v_ref = torch.tanh(fd.value_fc2(torch.relu(fd.value_fc1(torch.relu(fd.value_conv(xt)).flatten(1)))))
+    assert float((pf.double() - p_ref).abs().max()) <= 1e-4 * (float(p_ref.abs().max()) + 1.0)
+    assert float((v.double() - v_ref).abs().max()) <= 1e-4
+
+
+def _tower_ref(fd, obs):
+    x = torch.relu(fd.stem(obs))
+    h = x
+    for c1, c2 in fd.blocks:
+        h = c2(torch.relu(c1(h)))
+    return torch.relu(x + h)
