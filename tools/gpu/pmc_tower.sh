@@ -10,5 +10,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" 
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace -d $out/p$i -o c --output-format csv -- python tools/tower_bench.py 5 256 5 > $out/p$i.log 2>&1 || exit 1
 done
-python tools/pmc_to_json.py profiles/r01_pmc_tower.json k_tower_wino k_tower_wino 256 55050240 \
+python tools/pmc_to_json.py gpurun_out/r01_pmc_tower.json k_tower_wino k_tower_wino 256 55050240 \
   "rocprofv3 --pmc passes of tools/tower_bench.py (bk_resnet_tower, 256 boards 20x20, 10 convs 64->64); FETCH_SIZE doubled per the gfx950 correction, WRITE_SIZE as is; algorithmic bytes = tower input 26.2 MB + output 26.2 MB + 10 layers of Winograd U (262 KB each); the 9 intermediate activations (26.2 MB each way) stay on chip when L2 holds them" $out/p*
