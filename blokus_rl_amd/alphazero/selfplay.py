@@ -12,6 +12,7 @@ trajectories are statistically — not stream-for-stream — equivalent to np.ra
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -137,6 +138,7 @@ class SelfPlay:
         self.continuous = continuous
         self.mcts = BatchedMCTS(eng, games, node_cap=node_cap, child_cap=child_cap)
         self.evaluator = LeafEvaluator(model, eng, games, nn_dtype, use_graph)
+        self._use_graph = use_graph
         if getattr(self.evaluator, "planar", False) and self.evaluator.graph is not None:
             self.mcts.obs = self.evaluator.static_obs  # k_select writes the net's input buffer directly
         dev = eng.device
@@ -157,6 +159,10 @@ class SelfPlay:
         self._ensure_zcap()
         self._records: list[tuple[torch.Tensor, ...]] = []  # per-ply records (z resolved lazily)
         self.timers = None
+        self._fused_ok: bool | None = None
+        self._graph = None  # the captured simulations (_sim_graph)
+        # fused path: simulations per launch (0: all of a ply's in one launch)
+        self.sims_per_launch = int(os.environ.get("BK_SIMS_PER_LAUNCH", "0"))
         self._window: list[tuple[torch.Tensor, ...]] = []  # records since mark_window()
 
     @property
@@ -195,6 +201,71 @@ class SelfPlay:
         logp, v, mode = self._evaluate(obs)
         self.mcts.expand_backup(logp, v, prior_mode=mode)
 
+    SIM_GRAPH_SIMS = 10  # simulations per captured graph (paths without a fused kernel)
+
+    def fused(self) -> bool:
+        """Whole simulations in one launch (k_sims: the HIP ResNet in fp32 with the sparse policy
+        head; k_sims_const: DumbNet) unless stage timers are on or BK_SIM_FUSED=0."""
+        if self._fused_ok is None:
+            ev = self.evaluator
+            self._fused_ok = ev.model is None or bool(
+                ev.sparse and ev.dtype == torch.float32 and BatchedMCTS.fused_resnet_ok(self.eng, ev.model))
+        return self._fused_ok and self.timers is None and os.environ.get("BK_SIM_FUSED", "1") != "0"
+
+    def _simulations(self, n: int):
+        """n simulations of every active tree: fused launches (fused()), else replays of a graph of
+        SIM_GRAPH_SIMS captured simulations (no per-launch host work) and eager ones."""
+        if self.fused():
+            ev = self.evaluator
+            k = self.sims_per_launch if self.sims_per_launch > 0 else max(n, 1)
+            for s in range(0, n, k):
+                c = min(k, n - s)
+                if ev.model is None:
+                    self.mcts.simulate_const(self.roots, self.active, self.cpuct, c, ev.const_logp, ev.const_v)
+                else:
+                    self.mcts.simulate_resnet(self.roots, self.active, self.cpuct, c, ev.model)
+            return
+        k = self.SIM_GRAPH_SIMS
+        if n >= k and self._graph_usable():
+            g = self._sim_graph()
+            self._g_roots.copy_(self.roots)
+            self._g_active.copy_(self.active)
+            for _ in range(n // k):
+                g.replay()
+            n -= (n // k) * k
+        for _ in range(n):
+            self.simulate()
+
+    def _graph_usable(self) -> bool:
+        ev = self.evaluator
+        return (self.timers is None and self._use_graph and (ev.model is None or ev.graph is not None)
+                and os.environ.get("BK_SIM_GRAPH", "1") != "0")
+
+    def _sim_body(self):
+        """One simulation on the captured buffers (_g_roots, _g_active)."""
+        _, obs, _ = self.mcts.select(self._g_roots, self._g_active, self.cpuct)
+        ev = self.evaluator
+        if ev.model is None:
+            self.mcts.expand_backup(ev.const_logp, ev.const_v, prior_mode=0)
+            return
+        out, v = ev._forward(obs)
+        if ev.sparse:
+            self.mcts.leaf_logits(out, ev.policy_w, ev.policy_b)
+            self.mcts.expand_backup(None, v, prior_mode=2)
+        else:
+            self.mcts.expand_backup(out, v, prior_mode=0)
+
+    def _sim_graph(self):
+        if self._graph is None:
+            self._g_roots = self.roots.clone()
+            self._g_active = self.active.clone()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.SIM_GRAPH_SIMS):
+                    self._sim_body()
+            self._graph = g
+        return self._graph
+
     def enable_timers(self, on: bool = True):
         """HIP events around each stage on the launch stream (bench.py roofline inputs)."""
         self.timers = {"select": [], "net": [], "expand": []} if on else None
@@ -219,8 +290,7 @@ class SelfPlay:
 
     # ------------------------------------------------------------------ one ply
     def play_ply(self, record: bool = True):
-        for _ in range(self.num_sims):
-            self.simulate()
+        self._simulations(self.num_sims)
         ids, pi, counts = self.mcts.root_policy(self.roots, self.active, self.temperature, self.cap)
         G, cap = self.G, self.cap
         col = torch.arange(cap, device=self.eng.device).unsqueeze(0)

@@ -47,8 +47,6 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     torch.cuda.synchronize()
     c0 = sp.mcts.counters()
     sims0 = sp.stats.sims
-    if timers:
-        sp.enable_timers(True)
     sp.mark_window()
     gather = {}
     t0 = time.perf_counter()
@@ -72,10 +70,42 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     c1 = sp.check_counters() if hasattr(sp, "check_counters") else sp.mcts.check()
     done = sp.stats.sims - sims0
     delta = {k: c1[k] - c0[k] for k in c1 if k not in ("errors", "nodes", "children")}
-    ms = sp.timer_ms() if timers else {}
+    ms = stage_times(sp) if timers else {}
     if gather:
         ms["all_gather"] = gather
     return sp, eng, done, elapsed, delta, ms
+
+
+def stage_times(sp) -> dict:
+    """Stage times outside the timed region. Fused path: a ply's simulations timed with HIP events
+    on their stream ('k_sims' / 'k_sims_const': ms, launches, leaves expanded and, for the ResNet,
+    the MFMA FLOP of their leaf nets). Then one ply launched stage by stage with events around each
+    stage: select / net / expand ms per sim-step."""
+    out = {}
+    if sp.fused():
+        st = torch.cuda.current_stream(sp.eng.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0 = sp.mcts.counters()
+        e0.record(st)
+        sp._simulations(sp.num_sims)
+        e1.record(st)
+        torch.cuda.synchronize()
+        leaves = sp.mcts.counters()["expanded"] - c0["expanded"]
+        k = sp.sims_per_launch if sp.sims_per_launch > 0 else sp.num_sims
+        rec = {"ms": e0.elapsed_time(e1), "sims": sp.num_sims, "launches": -(-sp.num_sims // k), "leaves": leaves}
+        model = sp.evaluator.model
+        if model is not None:
+            N, convs = sp.eng.N, 2 * len(model.f.blocks)
+            per_leaf = 2.0 * 16 * 64 * 64 * (N // 2) ** 2 * convs + 2.0 * N * N * 64 * 9 * model.f.stem.in_channels
+            rec.update(convs=convs, flop_per_leaf=per_leaf, flop=per_leaf * leaves)
+            out["k_sims"] = rec
+        else:
+            out["k_sims_const"] = rec
+    sp.enable_timers(True)
+    sp.play_ply()
+    out.update(sp.timer_ms())
+    sp.enable_timers(False)
+    return out
 
 
 def time_leaf_conv(sp, reps: int = 5):
@@ -163,6 +193,7 @@ def bench_selfplay(args, world, rank):
     net_flops = RESNET_FLOPS_PER_LEAF * delta["expanded"] / steps_sim
     net_peak = FP32_PEAK if args.nn_dtype == "fp32" else FP16_PEAK
     conv = time_leaf_conv(sp) if args.nn_dtype == "fp32" else None
+    ks = ms.pop("k_sims", None)
     out = {
         "metric": "MCTS sims/sec on 20x20 Blokus (4 players, 256 games/GPU, 100 sims/move)",
         "value": sims / elapsed,
@@ -195,13 +226,27 @@ def bench_selfplay(args, world, rank):
     }
     if conv is not None:
         cms, cflop, dflop = conv["ms"], conv["flop"], conv["direct"]
-        out["roofline"] = {"bound": "mfma", "kernel": conv["kernel"],
+        out["tower_roofline"] = {"bound": "mfma", "kernel": conv["kernel"],
                            "achieved": cflop / (cms * 1e-3) / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
                            "frac": cflop / (cms * 1e-3) / FP32_PEAK, "traffic": None, "kernel_ms": cms,
                            "flop_per_launch": cflop, "units_per_launch": G,
                            "direct_conv_equiv_tflops": dflop / (cms * 1e-3) / 1e12,
                            "launches_per_sim_step": conv["launches"],
                            "share_of_sim_step": conv["launches"] * cms / (elapsed / steps_sim * 1e3)}
+        out["roofline"] = out["tower_roofline"]
     else:
         out["roofline"] = out["search_roofline"]
+    if ks is not None:
+        # the fused path: a ply's simulations are k_sims launches, the only kernel of the sim-steps;
+        # its FLOP = the MFMA work of the leaf nets (stem + Winograd tower) of the leaves it expanded
+        tf = ks["flop"] / (ks["ms"] * 1e-3)
+        out["roofline"] = {
+            "bound": "mfma",
+            "kernel": "k_sims (a ply's %d simulations in %d launch(es), one workgroup per tree: select, the leaf "
+                      "ResNet - stem + %d Winograd F(2x2,3x3) f32 MFMA convs + heads - the sparse policy head, "
+                      "expand/backup)" % (ks["sims"], ks["launches"], ks["convs"]),
+            "achieved": tf / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s", "frac": tf / FP32_PEAK,
+            "traffic": None, "kernel_ms": ks["ms"] / ks["launches"], "flop_per_launch": ks["flop"] / ks["launches"],
+            "units_per_launch": ks["leaves"] / ks["launches"], "flop_per_leaf": ks["flop_per_leaf"],
+            "launches_per_ply": ks["launches"], "share_of_ply": ks["ms"] / (elapsed / args.steps * 1e3)}
     return out

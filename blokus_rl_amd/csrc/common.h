@@ -105,6 +105,21 @@ __device__ __forceinline__ float wave_max_f(float x) {
   return readlane_f(x, kWave - 1);
 }
 
+// LDS handoff between the lanes of the one wave that owns a board, in the board-level helpers
+// below and the search's per-tree stages (mcts_dev.h). Their per-stage kernels are 64-thread
+// workgroups and keep the barrier; sims.hip runs those stages on one wave of a 4-wave workgroup
+// (the other waves wait elsewhere meanwhile) and defines BK_BOARD_SYNC() as wave_lds_sync(): a
+// wave's LDS operations complete in issue order, so only the compiler must be kept from moving
+// LDS accesses across the handoff.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+#ifndef BK_BOARD_SYNC
+#define BK_BOARD_SYNC() __syncthreads()
+#endif
+
 // Copy a 384-byte state global -> LDS (96 words; lanes 0..63 + 0..31).
 __device__ __forceinline__ void load_state(uint32_t* s, const uint32_t* g) {
   const int l = lane_id();
@@ -142,7 +157,7 @@ __device__ __forceinline__ bool compute_fa(const DevPreset& dp, const uint32_t* 
     fa[l] = (uint64_t)forb | ((uint64_t)anch << 32);
   }
   const bool any = __ballot((anch & ~forb) != 0u) != 0ull;
-  __syncthreads();
+  BK_BOARD_SYNC();
   return any;
 }
 
@@ -197,7 +212,7 @@ __device__ __forceinline__ void build_mask(const DevPreset& dp, const uint32_t* 
       }
     }
   }
-  __syncthreads();
+  BK_BOARD_SYNC();
 }
 
 // Does colour q have at least one legal placement? (early exit on the first hit)
@@ -264,7 +279,7 @@ __device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, in
     s[kWPieces + p] &= ~(1u << pc);
     s[kWPly] += 1u;
   }
-  __syncthreads();
+  BK_BOARD_SYNC();
   uint32_t flags = s[kWFlags];
   int next = -1;
   for (int d = 1; d <= dp.P; ++d) {
@@ -274,9 +289,9 @@ __device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, in
     flags |= 1u << (kFlagDeadShift + q);
   }
   if (next < 0) { flags |= kFlagOver; next = (p + 1) % dp.P; }
-  __syncthreads();
+  BK_BOARD_SYNC();
   if (l == 0) { s[kWFlags] = flags; s[kWToMove] = (uint32_t)next; }
-  __syncthreads();
+  BK_BOARD_SYNC();
   return 0;
 }
 

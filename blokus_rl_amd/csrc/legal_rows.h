@@ -115,9 +115,9 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
 #pragma unroll
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32;
-  __syncthreads();
+  BK_BOARD_SYNC();
   orient_all<1, 0>(dp, c, 0, std::make_index_sequence<kNumOrient>{});
-  __syncthreads();
+  BK_BOARD_SYNC();
 }
 
 // Workgroup = WPB waves sharing one group of boards_per_wave boards: wave w evaluates the

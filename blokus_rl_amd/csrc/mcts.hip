@@ -21,139 +21,9 @@
 #include "../../include/blokus_engine.h"
 #include "ctx.h"
 #include "legal_rows.h"
+#include "mcts_dev.h"
 
 namespace bk {
-
-constexpr int kMaxDepth = 96;
-constexpr int kExpandLdsIds = 2048;  // leaf ids staged in LDS up to this K
-constexpr int kGatherRegs = 16;      // logits gathered into registers: K <= 1024 in one round
-constexpr int kLeafCap = 2048;       // sparse leaf policy: legal ids per leaf (bk_mcts_leaf_logits)
-constexpr int kLeafBlocks = 4;       // workgroups per tree in k_leaf_logits
-constexpr int kMaxFeat = 2048;       // policy-feature length staged in LDS
-
-// Diagnostic build only (-DBK_STAMPS, `make diag`): per-tree s_memtime stamps at phase
-// boundaries of k_select / k_expand_backup; never compiled into the shipped library.
-#ifdef BK_STAMPS
-__device__ unsigned long long g_stamps[2][4096][8];
-#define BK_STAMP(k, i) \
-  do { if (lane_id() == 0 && blockIdx.x < 4096) g_stamps[k][blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define BK_STAMP(k, i) do { } while (0)
-#endif  // > 84 = most placements a 4-player game can still make
-
-struct DevMcts {
-  int T, node_cap, TS;  // TS = table slots per tree (power of two)
-  int64_t child_cap_per_tree;
-  uint64_t* tab_key;    // [T*TS] 0 = empty
-  int32_t* tab_node;    // [T*TS] tree-local node index
-  int32_t* tree_nodes;  // [T]
-  int64_t* tree_children;  // [T] children used in the tree's region
-  int64_t* node_child;  // [T*node_cap] offset into the child arrays (global index)
-  int32_t* node_K;      // [T*node_cap]
-  uint32_t* node_visits;  // [T*node_cap]  = sum of the children's N
-  int32_t* ch_id;       // [T*cpt]
-  uint32_t* ch_N;
-  double* ch_Q;
-  float* ch_P;
-  int32_t* path_node;   // [T*kMaxDepth] tree-local node
-  int64_t* path_child;  // [T*kMaxDepth] global child index
-  int32_t* path_pl;     // [T*kMaxDepth] player to move at the child (scores index)
-  int32_t* depth;       // [T]
-  uint32_t* leaf_state; // [T*kStateWords]
-  int32_t* leaf_status; // [T]
-  double* leaf_scores;  // [T*kMaxP]
-  uint64_t* leaf_mask;  // [T*W64] internal copy of the leaf bitmask
-  int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
-  float* leaf_logit;    // [T*kLeafCap] their logits
-  int32_t* leaf_K;      // [T]
-  unsigned long long* counters;  // [8]
-};
-
-enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5, kCtrScanned = 6, kCtrLeafK = 7 };
-enum { kErrChildPool = 1, kErrTable = 2, kErrDepth = 4, kErrIllegal = 8, kErrMissingRoot = 16, kErrLeafCap = 32 };
-
-__device__ __forceinline__ uint64_t table_key(const uint32_t* s) {
-  const uint64_t h = state_hash(s);
-  return h ? h : 1ull;
-}
-
-// Wave-parallel linear probe; returns the tree-local node or -1 (key absent).
-__device__ __forceinline__ int table_find(const DevMcts& m, int t, uint64_t key, int* free_slot) {
-  const int l = lane_id();
-  const uint32_t mask = (uint32_t)m.TS - 1u;
-  const uint32_t start = (uint32_t)(key ^ (key >> 29)) & mask;
-  const uint64_t* keys = m.tab_key + (size_t)t * m.TS;
-  for (int p0 = 0; p0 < m.TS; p0 += kWave) {
-    const uint32_t slot = (start + (uint32_t)(p0 + l)) & mask;
-    const uint64_t k = keys[slot];
-    const uint64_t hit = __ballot(k == key);
-    const uint64_t emp = __ballot(k == 0ull);
-    if (hit) {
-      const int src = __ffsll((unsigned long long)hit) - 1;
-      const int slot_hit = readlane_i((int)slot, src);
-      return m.tab_node[(size_t)t * m.TS + slot_hit];
-    }
-    if (emp) {
-      const int src = __ffsll((unsigned long long)emp) - 1;
-      if (free_slot) *free_slot = readlane_i((int)slot, src);
-      return -1;
-    }
-  }
-  if (free_slot) *free_slot = -1;
-  return -1;
-}
-
-// argmax over (value, index): larger value wins, ties -> smaller index (np.argmax's first max).
-// DPP prefix-argmax; lane 63 ends with the wave's argmax, returned uniform.
-__device__ __forceinline__ void wave_argmax(double& best, int& bi) {
-  const int l = lane_id(), rl = l & 15;
-#define BK_ARGMAX_STEP(CTRL, COND)                                 \
-  {                                                               \
-    const double tb = dpp_d<CTRL>(best);                          \
-    const int ti = dpp_i<CTRL>(bi);                               \
-    if ((COND) && (tb > best || (tb == best && ti < bi))) {        \
-      best = tb;                                                  \
-      bi = ti;                                                    \
-    }                                                             \
-  }
-  BK_ARGMAX_STEP(0x111, rl >= 1)
-  BK_ARGMAX_STEP(0x112, rl >= 2)
-  BK_ARGMAX_STEP(0x114, rl >= 4)
-  BK_ARGMAX_STEP(0x118, rl >= 8)
-  BK_ARGMAX_STEP(0x142, (l & 31) >= 16)
-  BK_ARGMAX_STEP(0x143, l >= 32)
-#undef BK_ARGMAX_STEP
-  bi = readlane_i(bi, kWave - 1);
-  const uint64_t u = readlane_u64((uint64_t)__double_as_longlong(best), kWave - 1);
-  best = __longlong_as_double((long long)u);
-}
-
-// PUCT choice at a node (mcts.py:41-46): argmax_i Q_i + cpuct*P_i*sqrt(sum N + 1e-6)/(1+N_i).
-__device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, uint32_t visits, double cp) {
-  const int l = lane_id();
-  const double sq = sqrt((double)visits + 1e-6);
-  double best = -INFINITY;
-  int bi = 0x7fffffff;
-  const float* P = m.ch_P + off;
-  const uint32_t* Nn = m.ch_N + off;
-  const double* Q = m.ch_Q + off;
-  int i = l;
-  for (; i + kWave < K; i += 2 * kWave) {  // two children per lane per trip: loads overlap
-    const float p0 = P[i], p1 = P[i + kWave];
-    const uint32_t n0 = Nn[i], n1 = Nn[i + kWave];
-    const double q0 = Q[i], q1 = Q[i + kWave];
-    const double h0 = q0 + ((cp * (double)p0) * sq) / (1.0 + (double)n0);
-    const double h1 = q1 + ((cp * (double)p1) * sq) / (1.0 + (double)n1);
-    if (h0 > best) { best = h0; bi = i; }
-    if (h1 > best) { best = h1; bi = i + kWave; }
-  }
-  if (i < K) {
-    const double h = Q[i] + ((cp * (double)P[i]) * sq) / (1.0 + (double)Nn[i]);
-    if (h > best) { best = h; bi = i; }
-  }
-  wave_argmax(best, bi);
-  return bi;
-}
 
 __global__ __launch_bounds__(64) void k_reset(DevMcts m, const int32_t* flags) {
   const int t = blockIdx.y;
@@ -163,326 +33,28 @@ __global__ __launch_bounds__(64) void k_reset(DevMcts m, const int32_t* flags) {
   if (i == 0) { m.tree_nodes[t] = 0; m.tree_children[t] = 0; }
 }
 
+// grid T x 64 threads: one wave per tree
 __global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
                                                const int32_t* __restrict__ active, double cpuct,
                                                int32_t* __restrict__ status_out, float* __restrict__ obs,
                                                uint64_t* __restrict__ mask_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* s = lds;
-  uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
-  uint32_t* m32 = lds + kStateWords + 2 * kMaxN;
-  const int t = blockIdx.x;
-  const int l = lane_id();
-  const int obs_len = 2 * dp.P * dp.N * dp.N;
-  if (active && !active[t]) {
-    if (l == 0) { m.leaf_status[t] = 0; status_out[t] = 0; m.depth[t] = 0; }
-    for (int i = l; i < obs_len; i += kWave) obs[(size_t)t * obs_len + i] = 0.0f;
-    return;
-  }
-  BK_STAMP(0, 0);
-  load_state(s, roots + (size_t)t * kStateWords);
-  __syncthreads();
-  BK_STAMP(0, 1);
-  double cp = cpuct;
-  int depth = 0, err = 0;
-  long long scanned = 0;
-  for (;;) {
-    const int node = table_find(m, t, table_key(s), nullptr);
-    if (node < 0) break;
-    const size_t gn = (size_t)t * m.node_cap + node;
-    const int64_t off = m.node_child[gn];
-    const int Kn = m.node_K[gn];
-    scanned += Kn;
-    const int ci = select_child(m, off, Kn, m.node_visits[gn], cp);
-    const int a = m.ch_id[off + ci];
-    if (depth >= kMaxDepth) { err |= kErrDepth; break; }
-    if (apply_action(dp, s, a, fa)) { err |= kErrIllegal; break; }
-    if (l == 0) {
-      const size_t pi = (size_t)t * kMaxDepth + depth;
-      m.path_node[pi] = node;
-      m.path_child[pi] = off + ci;
-      m.path_pl[pi] = (int)s[kWToMove];
-    }
-    ++depth;
-    cp = 1.0;  // the recursive call of mcts.py:50 passes no cpuct
-  }
-  BK_STAMP(0, 2);
-  int status;
-  float* o = obs + (size_t)t * obs_len;
-  if (err) {
-    status = 0;
-  } else if (s[kWFlags] & kFlagOver) {
-    status = 2;
-    if (l == 0) terminal_scores(dp, s, m.leaf_scores + (size_t)t * kMaxP);
-  } else {
-    status = 1;
-    build_mask_rows(dp, s, (int)s[kWToMove], m32);
-    BK_STAMP(0, 3);
-    uint64_t* mo = m.leaf_mask + (size_t)t * dp.W64;
-    uint64_t* mo2 = mask_out ? mask_out + (size_t)t * dp.W64 : nullptr;
-    for (int j = l; j < dp.W64; j += kWave) {
-      const uint64_t w = (uint64_t)m32[2 * j] | ((uint64_t)m32[2 * j + 1] << 32);
-      mo[j] = w;
-      if (mo2) mo2[j] = w;
-    }
-    store_state(m.leaf_state + (size_t)t * kStateWords, s);
-  }
-  BK_STAMP(0, 4);
-  // observation row (zeros unless the leaf needs the net): lane = (plane, board row), the row's
-  // N floats as float4 stores when N is a multiple of 4 (no per-cell index arithmetic)
-  const int tm = (int)s[kWToMove];
-  const int rows = 2 * dp.P * dp.N;
-  for (int pr = l; pr < rows; pr += kWave) {
-    const int plane = pr / dp.N, r = pr - plane * dp.N;
-    uint32_t bits = 0u;
-    if (status == 1) bits = plane < dp.P ? s[plane * kMaxN + r] : ((plane - dp.P) == tm ? dp.full_row : 0u);
-    float* dst = o + pr * dp.N;
-    if ((dp.N & 3) == 0) {
-      for (int c = 0; c < dp.N; c += 4)
-        *reinterpret_cast<float4*>(dst + c) = make_float4((float)((bits >> c) & 1u), (float)((bits >> (c + 1)) & 1u),
-                                                          (float)((bits >> (c + 2)) & 1u), (float)((bits >> (c + 3)) & 1u));
-    } else {
-      for (int c = 0; c < dp.N; ++c) dst[c] = (float)((bits >> c) & 1u);
-    }
-  }
-  BK_STAMP(0, 5);
-  if (l == 0) {
-    m.leaf_status[t] = status;
-    status_out[t] = status;
-    m.depth[t] = depth;
-    atomicAdd(&m.counters[kCtrLevels], (unsigned long long)depth);
-    atomicAdd(&m.counters[kCtrScanned], (unsigned long long)scanned);
-    if (status == 2) atomicAdd(&m.counters[kCtrTerminal], 1ull);
-    if (err) atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
-  }
+  select_tree(dp, m, blockIdx.x, roots, active, cpuct, status_out, obs, mask_out, lds);
 }
 
-// The policy head's last layer restricted to the leaf's legal ids (the only logits the
-// expansion reads): logit[j] = W[id_j] . feat[t] + bias[id_j] for the K legal ids of tree t's
-// leaf, instead of the dense [T, A] Linear (blokus_nnet.py:147-148) — K ~ 200 of A = 30433.
-// kLeafBlocks workgroups per tree each compact the leaf bitmask (ascending ids) and take a
-// contiguous share of the ids; a wave computes four dot products at a time (16 lanes each) over
-// the feature row staged in LDS, W rows read as coalesced float4s, several loads in flight.
+// grid (T, kLeafBlocks) x 256 threads: workgroup c takes share c of the tree's legal ids
 __global__ __launch_bounds__(256) void k_leaf_logits(DevPreset dp, DevMcts m, const float* __restrict__ feat,
                                                      int64_t ldf, int F, const float* __restrict__ W,
                                                      const float* __restrict__ bias) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* m32 = lds;                                                   // W32pad words
-  int32_t* ids = reinterpret_cast<int32_t*>(lds + dp.W32pad);            // kLeafCap
-  float* f = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap);       // F (16-B aligned: W32pad % 4 == 0)
-  __shared__ int Ksh;
-  const int t = blockIdx.x, c = blockIdx.y;
-  if (m.leaf_status[t] != 1) return;  // block-uniform: no leaf to evaluate
-  const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
-  for (int j = threadIdx.x; j < dp.W64; j += blockDim.x) {
-    const uint64_t w = lm[j];
-    m32[2 * j] = (uint32_t)w;
-    m32[2 * j + 1] = (uint32_t)(w >> 32);
-  }
-  const float* ft = feat + (size_t)t * ldf;
-  for (int i = threadIdx.x; i < F; i += blockDim.x) f[i] = ft[i];
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (wave == 0) {
-    const int K = compact_ids(dp, m32, ids, kLeafCap);
-    if (l == 0) Ksh = K;
-  }
-  __syncthreads();
-  const int K = Ksh;
-  if (c == 0 && threadIdx.x == 0) {
-    m.leaf_K[t] = K;
-    if (K > kLeafCap) atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrLeafCap);
-  }
-  if (K > kLeafCap) return;
-  const int lo = (int)((int64_t)K * c / kLeafBlocks), hi = (int)((int64_t)K * (c + 1) / kLeafBlocks);
-  int32_t* out_ids = m.leaf_ids + (size_t)t * kLeafCap;
-  float* out_lg = m.leaf_logit + (size_t)t * kLeafCap;
-  const int nw = blockDim.x >> 6;
-  if ((F & 3) == 0) {
-    // four ids per wave at a time, 16 lanes each: a lane streams every 16th float4 of its row
-    // (up to 4 loads in flight), the 16-lane partial sums meet in 4 xor-shuffles
-    const int F4 = F >> 2;
-    const float4* f4 = reinterpret_cast<const float4*>(f);
-    const int sub = l & 15, quad = l >> 4;
-    for (int j0 = lo + 4 * wave; j0 < hi; j0 += 4 * nw) {
-      const int j = j0 + quad;
-      const bool ok = j < hi;
-      const int id = ids[ok ? j : lo];
-      const float4* r = reinterpret_cast<const float4*>(W + (size_t)id * F);
-      float a0 = 0.f, a1 = 0.f;
-      int q = sub;
-      for (; q + 48 < F4; q += 64) {
-        const float4 w0 = r[q], w1 = r[q + 16], w2 = r[q + 32], w3 = r[q + 48];
-        const float4 x0 = f4[q], x1 = f4[q + 16], x2 = f4[q + 32], x3 = f4[q + 48];
-        a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
-        a1 += w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
-        a0 += w2.x * x2.x + w2.y * x2.y + w2.z * x2.z + w2.w * x2.w;
-        a1 += w3.x * x3.x + w3.y * x3.y + w3.z * x3.z + w3.w * x3.w;
-      }
-      for (; q < F4; q += 16) {
-        const float4 w0 = r[q], x0 = f4[q];
-        a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
-      }
-      float a = a0 + a1;
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
-      if (sub == 0 && ok) {
-        out_ids[j] = id;
-        out_lg[j] = a + bias[id];
-      }
-    }
-  } else {
-    for (int j = lo + wave; j < hi; j += nw) {
-      const int id = ids[j];
-      const float* r = W + (size_t)id * F;
-      float a = 0.f;
-      for (int q = l; q < F; q += kWave) a += r[q] * f[q];
-      a = wave_sum_f(a);
-      if (l == 0) {
-        out_ids[j] = id;
-        out_lg[j] = a + bias[id];
-      }
-    }
-  }
+  leaf_logits_tree<1>(dp, m, blockIdx.x, blockIdx.y, kLeafBlocks, feat, ldf, F, W, bias, lds);
 }
 
-// prior_mode 0: logp = the net's log-probabilities over all A ids -> masked log-softmax + exp
-//               (get_valid_dist, neural_network.py:159-173);
-// prior_mode 2: the sparse leaf logits of k_leaf_logits (ids + logits of the legal ids) ->
-//               the same softmax, no compaction or gather here;
-// prior_mode 1: logp holds the prior itself at the legal ids (test hook: identical P fed to the
-//               reference and to this engine).
+// grid T x 64 threads
 __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, const float* __restrict__ logp,
                                                       const float* __restrict__ values, int prior_mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* m32 = lds;  // W32pad words
-  __shared__ double vsh[kMaxP];
-  const int t = blockIdx.x;
-  const int l = lane_id();
-  const int status = m.leaf_status[t];
-  if (status == 0) return;
-  BK_STAMP(1, 0);
-  if (status == 1) {
-    const bool sparse = prior_mode == 2;
-    int err = 0;
-    const int node = m.tree_nodes[t];
-    const int64_t used = m.tree_children[t];
-    const int64_t room = m.child_cap_per_tree - used;
-    const int64_t off = (int64_t)t * m.child_cap_per_tree + used;
-    int32_t* ids_lds = reinterpret_cast<int32_t*>(m32 + dp.W32pad);
-    const int cap_lds = kExpandLdsIds;
-    int K;
-    bool in_lds;
-    BK_STAMP(1, 1);
-    if (sparse) {
-      K = m.leaf_K[t];
-      in_lds = true;  // the ids are in leaf_ids: write them into the child region below
-      if (K > kLeafCap) err |= kErrLeafCap;
-    } else {
-      const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
-      for (int j = l; j < dp.W64; j += kWave) {
-        const uint64_t w = lm[j];
-        m32[2 * j] = (uint32_t)w;
-        m32[2 * j + 1] = (uint32_t)(w >> 32);
-      }
-      __syncthreads();
-      // legal ids, ascending (np.where order, mcts.py:64): into LDS when K fits, else straight
-      // into the tree's child region
-      K = compact_ids(dp, m32, ids_lds, cap_lds);
-      in_lds = K <= cap_lds;
-      if (!in_lds)
-        K = compact_ids(dp, m32, m.ch_id + off, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
-      __syncthreads();
-    }
-    BK_STAMP(1, 2);
-    if (node >= m.node_cap) err |= kErrTable;
-    if (K > room) err |= kErrChildPool;
-    int free_slot = -1;
-    const uint64_t key = table_key(m.leaf_state + (size_t)t * kStateWords);
-    if (!err) {
-      const int found = table_find(m, t, key, &free_slot);
-      if (found >= 0 || free_slot < 0) err |= kErrTable;
-    }
-    BK_STAMP(1, 3);
-    if (!err) {
-      // dense modes gather logp[cid[i]]; the sparse mode reads its logits in id order
-      const float* lp = sparse ? m.leaf_logit + (size_t)t * kLeafCap : logp + (size_t)t * dp.A;
-      const int32_t* cid = sparse ? m.leaf_ids + (size_t)t * kLeafCap : (in_lds ? ids_lds : m.ch_id + off);
-      auto logit = [&](int i) { return sparse ? lp[i] : lp[cid[i]]; };
-      // all of a lane's gathers issued before any is used (K <= 64 * kGatherRegs)
-      float x[kGatherRegs];
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < kGatherRegs; ++j) {
-        const int i = l + j * kWave;
-        x[j] = i < K ? logit(i) : -INFINITY;
-      }
-#pragma unroll
-      for (int j = 0; j < kGatherRegs; ++j) mx = fmaxf(mx, x[j]);
-      for (int i = l + kGatherRegs * kWave; i < K; i += kWave) mx = fmaxf(mx, logit(i));
-      float lse = 0.0f;
-      if (prior_mode != 1) {
-        mx = wave_max_f(mx);
-        float sum = 0.0f;
-#pragma unroll
-        for (int j = 0; j < kGatherRegs; ++j) sum += l + j * kWave < K ? expf(x[j] - mx) : 0.0f;
-        for (int i = l + kGatherRegs * kWave; i < K; i += kWave) sum += expf(logit(i) - mx);
-        sum = wave_sum_f(sum);
-        lse = logf(sum);
-#pragma unroll
-        for (int j = 0; j < kGatherRegs; ++j) x[j] = expf((x[j] - mx) - lse);
-      }
-      // coalesced child initialisation: child i = (id, N 0, Q 0, P)
-#pragma unroll
-      for (int j = 0; j < kGatherRegs; ++j) {
-        const int i = l + j * kWave;
-        if (i < K) {
-          if (in_lds) m.ch_id[off + i] = cid[i];
-          m.ch_N[off + i] = 0u;
-          m.ch_Q[off + i] = 0.0;
-          m.ch_P[off + i] = x[j];
-        }
-      }
-      for (int i = l + kGatherRegs * kWave; i < K; i += kWave) {
-        const float xi = logit(i);
-        if (in_lds) m.ch_id[off + i] = cid[i];
-        m.ch_N[off + i] = 0u;
-        m.ch_Q[off + i] = 0.0;
-        m.ch_P[off + i] = prior_mode != 1 ? expf((xi - mx) - lse) : xi;
-      }
-      if (l == 0) {
-        const size_t gn = (size_t)t * m.node_cap + node;
-        m.node_child[gn] = off;
-        m.node_K[gn] = K;
-        m.node_visits[gn] = 0u;
-        m.tab_key[(size_t)t * m.TS + free_slot] = key;
-        m.tab_node[(size_t)t * m.TS + free_slot] = node;
-        m.tree_nodes[t] = node + 1;
-        m.tree_children[t] = used + K;
-        atomicAdd(&m.counters[kCtrExpanded], 1ull);
-        atomicAdd(&m.counters[kCtrLeafK], (unsigned long long)K);
-      }
-    } else if (l == 0) {
-      atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
-    }
-    if (l < dp.P) vsh[l] = (double)values[(size_t)t * dp.P + l];
-  } else {
-    if (l < dp.P) vsh[l] = m.leaf_scores[(size_t)t * kMaxP + l];
-  }
-  BK_STAMP(1, 4);
-  __syncthreads();
-  const int depth = m.depth[t];
-  for (int d = l; d < depth; d += kWave) {
-    const size_t pi = (size_t)t * kMaxDepth + d;
-    const int64_t ci = m.path_child[pi];
-    const double v = vsh[m.path_pl[pi]];
-    const uint32_t n = m.ch_N[ci];
-    const double q = m.ch_Q[ci];
-    m.ch_Q[ci] = ((double)n * q + v) / (double)(n + 1u);
-    m.ch_N[ci] = n + 1u;
-    m.node_visits[(size_t)t * m.node_cap + m.path_node[pi]] += 1u;
-  }
-  BK_STAMP(1, 5);
+  expand_tree(dp, m, blockIdx.x, logp, values, prior_mode, lds);
 }
 
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
@@ -556,12 +128,6 @@ __global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restri
 }  // namespace bk
 
 using namespace bk;
-
-struct bk_mcts {
-  bk_ctx* ctx = nullptr;
-  DevMcts d{};
-  std::vector<void*> allocs;
-};
 
 template <typename T>
 static int mcts_alloc(bk_mcts* m, T** p, size_t count) {

@@ -162,6 +162,29 @@ int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, in
 int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
                         void* stream);
 
+/* Whole simulations in one launch (sims.hip, k_sims): for every active tree, nsims x { select ->
+ * the leaf ResNet (stem, Winograd residual tower, heads) -> the policy Linear over the leaf's
+ * legal ids -> expand/backup (mode 2) }, one workgroup per tree, no grid-wide step between the
+ * stages; the trees of nsims rounds of bk_mcts_select, bk_resnet_stem_tower_heads,
+ * bk_mcts_leaf_logits and bk_mcts_expand_backup(mode 2), bitwise. Replaces the simulation loop
+ * `for _ in range(num_mcts_sims): tree.simulate(...)` (trainer.py:104-105, mcts_player.py:16-17;
+ * MCTS.simulate, mcts.py:13-71, with predict, neural_network.py:92-110, at each leaf). 14x14 or
+ * 20x20 boards, 4 players; nlayers and the weights as for bk_resnet_stem_tower_heads, policy_w
+ * [A][2NN] and policy_b [A] (policy_out, models/blokus_nnet.py:147); f32 scratch, 16-byte
+ * aligned: obs [T][8][N][N], x0 / hA / hB [T][N][N][64], pf [T][2NN], v [T][P]. */
+int bk_mcts_simulate_resnet(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int nsims,
+                            int nlayers, const float* wstem, const float* bstem, const float* u2all,
+                            const float* biasall, const float* wp, const float* bp, const float* wv,
+                            const float* bv, const float* w1t, const float* b1, const float* w2, const float* b2,
+                            const float* policy_w, const float* policy_b, float* obs, float* x0, float* hA,
+                            float* hB, float* pf, float* v, void* stream);
+
+/* The same with a leaf evaluation that does not depend on the leaf (DumbNet, compare_arena.py:87-95:
+ * logp [T][A] and values [T][P] for every leaf of tree t), k_sims_const, one wave per tree: the
+ * trees of nsims rounds of bk_mcts_select + bk_mcts_expand_backup(logp, values, 0). */
+int bk_mcts_simulate_const(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int nsims,
+                           const float* logp, const float* values, void* stream);
+
 /* get_distribution (mcts.py:73-99) at the root of every active tree: ids[t][0..K) and
  * pi[t][0..K) (f64) in child order, K in counts[t]; temperature 0 -> one-hot argmax N
  * (first max); all-zero N -> uniform. Rows are `cap` wide. Root must be expanded. */
