@@ -205,12 +205,14 @@ class SelfPlay:
 
     def fused(self) -> bool:
         """Whole simulations in one launch (k_sims: the HIP ResNet in fp32 with the sparse policy
-        head; k_sims_const: DumbNet) unless stage timers are on or BK_SIM_FUSED=0."""
+        head; k_sims_const: DumbNet) when BK_SIM_FUSED=1 and no stage timers are on. Off by default:
+        bitwise the same trees, but measured slower than the per-stage launches replayed from a HIP
+        graph (round 1: 423k vs 555k sims/s at config 3)."""
         if self._fused_ok is None:
             ev = self.evaluator
             self._fused_ok = ev.model is None or bool(
                 ev.sparse and ev.dtype == torch.float32 and BatchedMCTS.fused_resnet_ok(self.eng, ev.model))
-        return self._fused_ok and self.timers is None and os.environ.get("BK_SIM_FUSED", "1") != "0"
+        return self._fused_ok and self.timers is None and os.environ.get("BK_SIM_FUSED", "0") == "1"
 
     def _simulations(self, n: int):
         """n simulations of every active tree: fused launches (fused()), else replays of a graph of

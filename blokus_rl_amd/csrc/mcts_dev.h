@@ -288,7 +288,7 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
   int32_t* out_ids = m.leaf_ids + (size_t)t * kLeafCap;
   float* out_lg = m.leaf_logit + (size_t)t * kLeafCap;
   const int nw = blockDim.x >> 6;
-  if ((F & 3) == 0 && F <= 64 * kLeafQ) {
+  if (R > 1 && (F & 3) == 0 && F <= 64 * kLeafQ) {
     // R x four ids per wave at a time, 16 lanes each: a lane holds every 16th float4 of each of its
     // R rows (<= kLeafQ a row), all loads issued before the first is used — one memory round trip
     // per R x 4 ids — then sums them in the order of the streaming loop below (the same logits,

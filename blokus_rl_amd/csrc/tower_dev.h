@@ -81,10 +81,7 @@ struct W2Lane {
   // parts k = (h, i): row i of the 4x4 result, t_i = (B^T d)_i from two window rows, v_i = t_i B
   __device__ void transform_part(const f32x4 (&raw)[16], int buf, int k) const {
     const int h = k >> 2, i = k & 3;
-    // within a (k-step, position) row of 64 floats, odd k-steps are rotated by 2 floats: the two
-    // channel quads of a half-wave's b64 writes then cover all 64 banks (no 2-way conflict); the
-    // readers (w2_group) rotate the same way
-    float* dst = v_lds + buf * kW2VBuf + sq * 1024 + ((tt * 4 + 2 * h + 2 * (sq & 1)) & 63);
+    float* dst = v_lds + buf * kW2VBuf + sq * 1024 + tt * 4 + 2 * h;
     auto d = [&](int q) { return h ? raw[q].zw : raw[q].xy; };
     f32x2 t[4];
 #pragma unroll
@@ -246,14 +243,11 @@ template <int MODE, bool WINDOW_IN_RAW = (MODE == kW2First), class NextWindow>
 __device__ __forceinline__ void w2_group(const W2Lane& c, f32x4 (&ur)[64], f32x4 (&raw)[16], const f32x4* usrc,
                                          const f32x4* unext, __amdgpu_buffer_rsrc_t xr_next, f32x4 bias4, int buf,
                                          NextWindow next_window, f32x4 (&acc)[16]) {
-  // V[buf][s][p][t][g], odd k-steps s rotated by 2 floats within a row (W2Lane::transform_part)
-  const int lo = (c.l & 15) * 4 + (c.l >> 4);
-  const float* vsrc0 = c.v_lds + buf * kW2VBuf + lo;
-  const float* vsrc1 = c.v_lds + buf * kW2VBuf + ((lo + 2) & 63);
+  const float* vsrc = c.v_lds + buf * kW2VBuf + (c.l & 15) * 4 + (c.l >> 4);  // V[buf][s][p][t][g]
   float vb[2][16];
   unsigned off[16];
 #pragma unroll
-  for (int p = 0; p < 16; ++p) vb[0][p] = vsrc0[p * 64];
+  for (int p = 0; p < 16; ++p) vb[0][p] = vsrc[p * 64];
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
     if (s == 0 && !WINDOW_IN_RAW) next_window(off);
@@ -271,7 +265,7 @@ __device__ __forceinline__ void w2_group(const W2Lane& c, f32x4 (&ur)[64], f32x4
     }
     if (s + 1 < 16) {  // B operands of the next k-step, before any VALU work of this one
 #pragma unroll
-      for (int p = 0; p < 16; ++p) vb[(s + 1) & 1][p] = ((s + 1) & 1 ? vsrc1 : vsrc0)[((s + 1) * 16 + p) * 64];
+      for (int p = 0; p < 16; ++p) vb[(s + 1) & 1][p] = vsrc[((s + 1) * 16 + p) * 64];
     }
     __builtin_amdgcn_sched_barrier(0);
     if (s >= 8) c.transform_part(raw, buf ^ 1, s - 8);
