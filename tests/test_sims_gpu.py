@@ -44,7 +44,8 @@ def test_fused_simulations_match_stagewise(T, sims):
         assert torch.equal(x, y)
     s1, d1 = m1.leaf_info()
     s2, d2 = m2.leaf_info()
-    assert torch.equal(s1, s2) and torch.equal(d1, d2)
+    a = active.bool()  # an inactive tree's leaf-state row is never written (uninitialised memory)
+    assert torch.equal(s1[a], s2[a]) and torch.equal(d1, d2)
 
 
 @pytest.mark.parametrize("fused,graph", [("1", "1"), ("0", "1")])
