@@ -55,6 +55,21 @@ __device__ __forceinline__ void wave_handoff() {
   asm volatile("buffer_inv sc0" ::: "memory");
 }
 
+// The search stages as out-of-line calls inside k_sims: inlined next to the tower they pushed the
+// kernel's register allocation into 3 KB/lane of scratch (the tower's U array is 256 AGPRs).
+__device__ __noinline__ int sims_select(const DevPreset& dp, const DevMcts& m, int t, const uint32_t* roots,
+                                        const int32_t* active, double cpuct, float* obs, uint32_t* lds) {
+  return select_tree(dp, m, t, roots, active, cpuct, nullptr, obs, nullptr, lds);
+}
+__device__ __noinline__ void sims_leaf_logits(const DevPreset& dp, const DevMcts& m, int t, const float* feat, int F,
+                                              const float* W, const float* bias, uint32_t* lds) {
+  leaf_logits_tree<2>(dp, m, t, 0, 1, feat, F, F, W, bias, lds);
+}
+__device__ __noinline__ void sims_expand(const DevPreset& dp, const DevMcts& m, int t, const float* values,
+                                         uint32_t* lds) {
+  expand_tree(dp, m, t, nullptr, values, 2, lds);
+}
+
 template <int N>
 __global__ __launch_bounds__(kW2Threads, 1) void k_sims(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
                                                         const int32_t* __restrict__ active, double cpuct, int nsims,
@@ -66,7 +81,7 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_sims(DevPreset dp, DevMcts m,
   constexpr int F = 2 * N * N;
   for (int sim = 0; sim < nsims; ++sim) {
     if (wave == 0) {
-      const int st = select_tree(dp, m, t, roots, active, cpuct, nullptr, const_cast<float*>(net.hd.obs), nullptr, lds32);
+      const int st = sims_select(dp, m, t, roots, active, cpuct, const_cast<float*>(net.hd.obs), lds32);
       if (threadIdx.x == 0) status_sh = st;
     }
     wg_handoff();
@@ -74,10 +89,10 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_sims(DevPreset dp, DevMcts m,
     if (status == 1) {
       tower_forward<N, true, true>(lds, net.x0, net.hA, net.hB, nullptr, net.u2all, net.biasall, net.nlayers, net.hd);
       wg_handoff();
-      leaf_logits_tree<2>(dp, m, t, 0, 1, net.hd.pf, F, F, net.W, net.bias, lds32);
+      sims_leaf_logits(dp, m, t, net.hd.pf, F, net.W, net.bias, lds32);
       wg_handoff();
     }
-    if (wave == 0 && status != 0) expand_tree(dp, m, t, nullptr, net.hd.v, 2, lds32);
+    if (wave == 0 && status != 0) sims_expand(dp, m, t, net.hd.v, lds32);
     wg_handoff();
   }
 }
