@@ -207,7 +207,7 @@ class SelfPlay:
         """Whole simulations in one launch (k_sims: the HIP ResNet in fp32 with the sparse policy
         head; k_sims_const: DumbNet) when BK_SIM_FUSED=1 and no stage timers are on. Off by default:
         bitwise the same trees, but measured slower than the per-stage launches replayed from a HIP
-        graph (round 1: 459k vs 557k sims/s at config 3)."""
+        graph (round 1: 508k vs 557k sims/s at config 3)."""
         if self._fused_ok is None:
             ev = self.evaluator
             self._fused_ok = ev.model is None or bool(

@@ -71,6 +71,11 @@ __device__ __noinline__ void sims_expand(const DevPreset& dp, const DevMcts& m, 
 }
 
 template <int N>
+__device__ __noinline__ void sims_tower(float* lds, const SimNet& net) {
+  tower_forward<N, true, true>(lds, net.x0, net.hA, net.hB, nullptr, net.u2all, net.biasall, net.nlayers, net.hd);
+}
+
+template <int N>
 __global__ __launch_bounds__(kW2Threads, 1) void k_sims(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
                                                         const int32_t* __restrict__ active, double cpuct, int nsims,
                                                         SimNet net) {
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(kW2Threads, 1) void k_sims(DevPreset dp, DevMcts m,
     wg_handoff();
     const int status = status_sh;
     if (status == 1) {
-      tower_forward<N, true, true>(lds, net.x0, net.hA, net.hB, nullptr, net.u2all, net.biasall, net.nlayers, net.hd);
+      sims_tower<N>(lds, net);
       wg_handoff();
       sims_leaf_logits(dp, m, t, net.hd.pf, F, net.W, net.bias, lds32);
       wg_handoff();
