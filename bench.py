@@ -398,7 +398,8 @@ def main():
     ap.add_argument("--sims", type=int, default=100)
     ap.add_argument("--model", default="resnet", choices=["resnet", "dumbnet", "dcnnet"])
     ap.add_argument("--nn-dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--node-cap", type=int, default=8192)
+    ap.add_argument("--node-cap", type=int, default=None,
+                    help="nodes per tree (default: sims x the longest game + 1, SelfPlay.node_cap_for)")
     args = ap.parse_args()
     world, rank, _ = _dist_init()
     if args.workload == "legal":

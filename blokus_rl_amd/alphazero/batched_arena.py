@@ -47,13 +47,17 @@ def seat_of(player) -> ArenaSeat:
 
 
 class BatchedArena:
-    def __init__(self, eng: Engine, seats: list, cpuct: float = 1.0, node_cap: int = 4096,
+    def __init__(self, eng: Engine, seats: list, cpuct: float = 1.0, node_cap: int | None = None,
                  child_cap_per_tree: int | None = None, nn_dtype: torch.dtype = torch.float32):
         self.eng = eng
         self.seats = [s if isinstance(s, ArenaSeat) else seat_of(s) for s in seats]
         if len(self.seats) != eng.P:
             raise ValueError(f"{eng.P} players expected, got {len(self.seats)}")
         self.cpuct = cpuct
+        if node_cap is None:
+            # a seat's tree lives for the whole game and grows by <= sims nodes on each of its
+            # player's plies (at most num_pieces of them)
+            node_cap = max(s.simulations for s in self.seats) * eng.num_pieces + 1
         self.node_cap = node_cap
         self.child_cap_per_tree = child_cap_per_tree or node_cap * (256 if eng.N >= 14 else 64)
         self.nn_dtype = nn_dtype
@@ -121,7 +125,10 @@ class BatchedArena:
             act_t[tree] = (~over).to(torch.int32)
             ids, pi, counts = mcts.root_policy(roots, act_t, 0.0)
             ids_g, pi_g = ids.index_select(0, tree), pi.index_select(0, tree)
-            k = counts.index_select(0, tree).clamp(min=0)
+            k = counts.index_select(0, tree)
+            if bool(((k < 0) & ~over).any()):
+                raise RuntimeError("arena: a root had more children than the root_policy cap")
+            k = k.clamp(min=0)
             col = torch.arange(pi_g.shape[1], device=dev).unsqueeze(0)
             pi_g = torch.where(col < k.unsqueeze(1), pi_g, torch.full_like(pi_g, -1.0))
             best = pi_g.argmax(dim=1)  # first max, as np.argmax over the one-hot distribution
@@ -146,7 +153,7 @@ class BatchedArena:
 
 
 def play_match_batched(game, players: list, games_num: int, permute: bool = False, cpuct: float = 1.0,
-                       node_cap: int = 4096):
+                       node_cap: int | None = None):
     """play_match(game, players, games_num, permute) (arena.py:10-32) for MCTSPlayer seats,
     batched: -> (scores, items) with items[i] = {"scores": game i's one-hot, "frames": []}."""
     arena = BatchedArena(game.engine, players, cpuct=cpuct, node_cap=node_cap)

@@ -124,7 +124,7 @@ class LeafEvaluator:
 class SelfPlay:
     def __init__(self, eng: Engine, model: torch.nn.Module | None, games: int, num_sims: int = 100,
                  cpuct: float = 1.0, temperature: float = 1.0, dirichlet_alpha: float = 1.0,
-                 dirichlet_weight: float = 0.25, node_cap: int = 8192, child_cap: int | None = None,
+                 dirichlet_weight: float = 0.25, node_cap: int | None = None, child_cap: int | None = None,
                  cap: int = 2048, seed: int = 0, nn_dtype: torch.dtype = torch.float32, use_graph: bool = True,
                  continuous: bool = False):
         self.eng = eng
@@ -136,6 +136,8 @@ class SelfPlay:
         self.weight = dirichlet_weight
         self.cap = cap
         self.continuous = continuous
+        if node_cap is None:
+            node_cap = self.node_cap_for(eng, num_sims)
         self.mcts = BatchedMCTS(eng, games, node_cap=node_cap, child_cap=child_cap)
         self.evaluator = LeafEvaluator(model, eng, games, nn_dtype, use_graph)
         self._use_graph = use_graph
@@ -164,6 +166,31 @@ class SelfPlay:
         # fused path: simulations per launch (0: all of a ply's in one launch)
         self.sims_per_launch = int(os.environ.get("BK_SIMS_PER_LAUNCH", "0"))
         self._window: list[tuple[torch.Tensor, ...]] = []  # records since mark_window()
+        # an active game whose root had more children than `cap` (k_root returns counts = -K):
+        # latched on the device, raised by check() at the next host sync
+        self._cap_overflow = torch.zeros((), dtype=torch.int32, device=dev)
+
+    @staticmethod
+    def max_game_plies(eng: Engine) -> int:
+        """Upper bound on the plies of one game: every ply places one of a player's pieces."""
+        return eng.num_pieces * eng.P
+
+    @classmethod
+    def node_cap_for(cls, eng: Engine, num_sims: int) -> int:
+        """Nodes one tree can need over a whole game. A tree lives for one game (trainer.py:95)
+        and a simulation adds at most one node, so num_sims x plies + 1 (the first root) bounds it."""
+        return int(num_sims) * cls.max_game_plies(eng) + 1
+
+    def check(self) -> dict:
+        """Raise EngineError if any tree ran out of nodes/children (the search would otherwise
+        keep re-selecting an unexpanded leaf and distort pi) or a root had more than `cap`
+        children (the ply would be dropped). Synchronises the stream; returns the MCTS counters."""
+        from ..engine import EngineError
+
+        c = self.mcts.check()
+        if int(self._cap_overflow.item()):
+            raise EngineError(f"a root had more than cap={self.cap} children: raise SelfPlay(cap=...)")
+        return c
 
     @property
     def stats(self) -> SelfPlayStats:
@@ -298,6 +325,7 @@ class SelfPlay:
         col = torch.arange(cap, device=self.eng.device).unsqueeze(0)
         valid = col < counts.clamp(min=0).unsqueeze(1)
         pi = torch.where(valid, pi, torch.zeros_like(pi))
+        self._cap_overflow |= ((counts < 0) & self.active.bool()).any().to(torch.int32)
         # root-only Dirichlet noise on each game's first ply (trainer.py:110-116); drawn every
         # ply and applied where first_ply, so no host round trip decides it
         gam = torch._standard_gamma(torch.full((G, cap), self.alpha, dtype=torch.float64,
@@ -378,6 +406,7 @@ class SelfPlay:
             self.play_ply()
         torch.cuda.synchronize(self.eng.device)
         self._stats.seconds += time.perf_counter() - t0
+        self.check()
         return self.stats
 
     def examples(self, drain: bool = False) -> Examples | None:

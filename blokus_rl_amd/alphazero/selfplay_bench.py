@@ -67,7 +67,7 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    c1 = sp.check_counters() if hasattr(sp, "check_counters") else sp.mcts.check()
+    c1 = sp.check()  # raises on a node/child-table overflow or a root above cap
     done = sp.stats.sims - sims0
     delta = {k: c1[k] - c0[k] for k in c1 if k not in ("errors", "nodes", "children")}
     ms = stage_times(sp) if timers else {}

@@ -15,7 +15,7 @@
 from __future__ import annotations
 
 from pathlib import Path
-from pickle import Pickler, Unpickler
+from pickle import Pickler
 
 import numpy as np
 import torch
@@ -168,11 +168,12 @@ class AlphaZeroTrainer:
             Pickler(f).dump(examples)
 
     def _load_examples(self):
+        """Legacy `.examples` files of the last history window, through the allow-list unpickler
+        (replay_io.load_legacy): the directory may hold files this process did not write."""
         data = []
         files = sorted(Path(self.hparams.data_dir).rglob("*.examples"))
         for fp in files[-self.hparams.num_iters_for_train_examples_history:]:
-            with open(fp, "rb") as f:  # files this trainer wrote itself
-                data.extend(Unpickler(f).load())
+            data.extend(rio.load_legacy(fp))
         return data
 
     def _train_epochs(self, data):

@@ -563,17 +563,11 @@ int tower_launch(const float* x0, int B, int N, int nlayers, const float* u2all,
   if (B == 0) return BK_OK;
   // V buffers (128 KB), then the heads' per-pixel partials [NN][4 waves][3]
   const int lds = (int)(sizeof(float) * (2 * kW2VBuf + (hd ? N * N * 12 : 0)));
-  static bool attr = false;
-  if (!attr) {
+  {
     const void* fns[6] = {(const void*)k_tower_wino<14, false>, (const void*)k_tower_wino<20, false>,
                           (const void*)k_tower_wino<14, true>,  (const void*)k_tower_wino<20, true>,
                           (const void*)k_tower_wino<14, true, true>, (const void*)k_tower_wino<20, true, true>};
-    for (const void* fn : fns)
-      if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(sizeof(float) * (2 * kW2VBuf + 20 * 20 * 12))),
-                    "hipFuncSetAttribute") != BK_OK)
-        return BK_EHIP;
-    attr = true;
+    if (set_max_dynamic_lds(fns, 6, (int)(sizeof(float) * (2 * kW2VBuf + 20 * 20 * 12))) != BK_OK) return BK_EHIP;
   }
   hipStream_t s = (hipStream_t)stream;
   const TowerHeads h = hd ? *hd : TowerHeads{};
@@ -652,28 +646,18 @@ int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, cons
   const f32x4* wp = reinterpret_cast<const f32x4*>(wpacked);
   hipStream_t s = (hipStream_t)stream;
   if (cin == 64) {
-    static bool attr_set = false;
-    if (!attr_set) {  // 147 KB of dynamic LDS (above the 64 KB default)
+    {  // 147 KB of dynamic LDS (above the 64 KB default)
       const int bytes = (int)(sizeof(f32x4) * 9 * 16 * kWave);
       const void* fns[4] = {(const void*)k_conv3x3<64, 4, true, true>, (const void*)k_conv3x3<64, 4, true, false>,
                             (const void*)k_conv3x3<64, 4, false, true>, (const void*)k_conv3x3<64, 4, false, false>};
-      for (const void* fn : fns)
-        if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes),
-                      "hipFuncSetAttribute") != BK_OK)
-          return BK_EHIP;
-      attr_set = true;
+      if (set_max_dynamic_lds(fns, 4, bytes) != BK_OK) return BK_EHIP;
     }
     if (bk_conv3x3_form(N, cin) == 1 && !wino_form1()) {
-      static bool w2attr = false;
       const int lds = (int)(sizeof(float) * 2 * kW2VBuf);
-      if (!w2attr) {
+      {
         const void* fns[4] = {(const void*)k_conv3x3_wino2<true, true>, (const void*)k_conv3x3_wino2<true, false>,
                               (const void*)k_conv3x3_wino2<false, true>, (const void*)k_conv3x3_wino2<false, false>};
-        for (const void* fn : fns)
-          if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
-                        "hipFuncSetAttribute") != BK_OK)
-            return BK_EHIP;
-        w2attr = true;
+        if (set_max_dynamic_lds(fns, 4, lds) != BK_OK) return BK_EHIP;
       }
       BK_REQUIRE(total * 64 < (1ll << 31), "bk_conv3x3: batch too large");
       const float* u2 = wpacked + 9 * 64 * kCout + 2 * kWinoHalf;
@@ -694,16 +678,11 @@ int bk_conv3x3(const float* x, int B, int N, int cin, const float* wpacked, cons
       return launch_check("k_conv3x3_wino2");
     }
     if (bk_conv3x3_form(N, cin) == 1) {
-      static bool wattr = false;
       const int lds = (int)(sizeof(float) * kWinoHalf);
-      if (!wattr) {
+      {
         const void* fns[4] = {(const void*)k_conv3x3_wino<kWinoKB, true, true>, (const void*)k_conv3x3_wino<kWinoKB, true, false>,
                               (const void*)k_conv3x3_wino<kWinoKB, false, true>, (const void*)k_conv3x3_wino<kWinoKB, false, false>};
-        for (const void* fn : fns)
-          if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
-                        "hipFuncSetAttribute") != BK_OK)
-            return BK_EHIP;
-        wattr = true;
+        if (set_max_dynamic_lds(fns, 4, lds) != BK_OK) return BK_EHIP;
       }
       BK_REQUIRE(total * 64 < (1ll << 31), "bk_conv3x3: batch too large");
       const float* uw = wpacked + 9 * 64 * kCout;

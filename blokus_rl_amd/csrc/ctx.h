@@ -22,6 +22,9 @@ void set_error(const std::string& msg);
 int hip_check(hipError_t e, const char* what);
 // Launch-error check after a kernel launch.
 int launch_check(const char* what);
+// Raise the dynamic-LDS limit of kernels fns[0..n) to `bytes` on the current device, once per
+// (device, kernel); thread-safe.
+int set_max_dynamic_lds(const void* const* fns, int n, int bytes);
 }  // namespace bk
 
 #define BK_REQUIRE(cond, msg)            \

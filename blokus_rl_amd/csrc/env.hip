@@ -1,7 +1,10 @@
 // env.hip — batched Blokus rules engine on gfx950 + the env half of the C-ABI
 // (include/blokus_engine.h). One 64-lane wave per board; see common.h.
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <string>
+#include <utility>
 
 #include <cstdlib>
 
@@ -19,6 +22,24 @@ int hip_check(hipError_t e, const char* what) {
   return BK_EHIP;
 }
 int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
+
+int set_max_dynamic_lds(const void* const* fns, int n, int bytes) {
+  // The attribute belongs to the kernel on the current device: remember (device, kernel) pairs
+  // already raised, under a lock (several host threads may launch on several devices).
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  if (hip_check(hipGetDevice(&dev), "hipGetDevice") != BK_OK) return BK_EHIP;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < n; ++i) {
+    if (done.count({dev, fns[i]})) continue;
+    if (hip_check(hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes),
+                  "hipFuncSetAttribute") != BK_OK)
+      return BK_EHIP;
+    done.insert({dev, fns[i]});
+  }
+  return BK_OK;
+}
 
 namespace {
 

@@ -148,15 +148,9 @@ extern "C" int bk_mcts_simulate_resnet(bk_mcts* m, const void* roots, const int3
                  sizeof(uint32_t) * ((size_t)dp.W32pad + kExpandLdsIds) <= lds && F <= kMaxFeat &&
                  F <= 64 * kLeafQ,
              "bk_mcts_simulate_resnet: stage buffers exceed the LDS");
-  static bool attr = false;
-  if (!attr) {
+  {
     const void* fns[2] = {(const void*)k_sims<14>, (const void*)k_sims<20>};
-    for (const void* fn : fns)
-      if (hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(sizeof(float) * (2 * kW2VBuf + 20 * 20 * 12))),
-                    "hipFuncSetAttribute") != BK_OK)
-        return BK_EHIP;
-    attr = true;
+    if (set_max_dynamic_lds(fns, 2, (int)(sizeof(float) * (2 * kW2VBuf + 20 * 20 * 12))) != BK_OK) return BK_EHIP;
   }
   if (nsims == 0) return BK_OK;
   SimNet net{};

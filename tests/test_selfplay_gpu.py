@@ -91,3 +91,31 @@ def test_sparse_policy_head_matches_dense_priors():
     i2, n2, q2, p2, k2 = m2.root_stats(roots)
     assert torch.equal(k1, k2) and torch.equal(i1, i2)
     assert (p1 - p2).abs().max().item() < 1e-6
+
+
+def test_selfplay_raises_on_node_table_overflow():
+    """A tree that runs out of nodes must stop the run: run() checks the counters."""
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine, EngineError
+    from blokus_rl_amd.nets import DumbNet
+
+    eng = Engine(7, 2, 5)
+    sp = SelfPlay(eng, DumbNet(7, 2, eng.A), 4, num_sims=12, node_cap=8, seed=3)
+    with pytest.raises(EngineError):
+        sp.run(4)
+    # the default capacity is the whole-game bound and a full run stays clean
+    sp = SelfPlay(eng, DumbNet(7, 2, eng.A), 4, num_sims=12, seed=3)
+    assert sp.mcts.node_cap == 12 * eng.num_pieces * 2 + 1
+    sp.run(60)
+    assert sp.stats.games_finished == 4
+
+
+def test_selfplay_raises_when_root_exceeds_cap():
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine, EngineError
+    from blokus_rl_amd.nets import DumbNet
+
+    eng = Engine(7, 2, 5)
+    sp = SelfPlay(eng, DumbNet(7, 2, eng.A), 4, num_sims=4, cap=8, seed=3)  # 7x7 first move: > 8 ids
+    with pytest.raises(EngineError):
+        sp.run(2)

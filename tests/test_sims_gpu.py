@@ -16,16 +16,17 @@ def _leaf_model(eng, blocks=2, seed=0):
     return LeafResNet(net, normalize=False, features=True).eval()
 
 
-@pytest.mark.parametrize("T,sims", [(12, 9), (5, 3)])
-def test_fused_simulations_match_stagewise(T, sims):
+@pytest.mark.parametrize("N,T,sims", [(20, 12, 9), (20, 5, 3), (14, 7, 6)])
+def test_fused_simulations_match_stagewise(N, T, sims):
+    """k_sims<20> and k_sims<14> (the two board sizes the fused tower supports)."""
     from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
     from blokus_rl_amd.boards import random_boards
     from blokus_rl_amd.engine import Engine
 
-    eng = Engine(20, 4, 5)
+    eng = Engine(N, 4, 5)
     model = _leaf_model(eng)
     assert BatchedMCTS.fused_resnet_ok(eng, model)
-    roots = random_boards(eng, T, seed0=9, max_plies=24)
+    roots = random_boards(eng, T, seed0=9, max_plies=24 if N == 20 else 12)
     active = torch.ones(T, dtype=torch.int32, device=eng.device)
     active[T // 2] = 0
     kw = dict(node_cap=64, child_cap=T * 64 * 700)
