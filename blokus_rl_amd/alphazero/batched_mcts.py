@@ -75,10 +75,11 @@ class BatchedMCTS:
     @staticmethod
     def fused_resnet_ok(eng: Engine, model) -> bool:
         """simulate_resnet's net: a HIP nets.LeafResNet with the 8-plane stem (4 players), at least one
-        residual block and a board size the fused tower supports (14, 20)."""
-        from ..nets import LeafResNet, tower_enabled
+        residual block and a board size the fused tower supports (14, 20); k_sims runs the f32
+        tower, so only when the staged path runs it too (BK_NET_MATH=f32)."""
+        from ..nets import LeafResNet, net_math, tower_enabled
 
-        return (isinstance(model, LeafResNet) and model.native and model.f.stem.in_channels == 8
+        return (net_math() == "f32" and isinstance(model, LeafResNet) and model.native and model.f.stem.in_channels == 8
                 and len(model.f.blocks) > 0 and tower_enabled() and bool(eng.lib.bk_tower_supported(eng.N)))
 
     def simulate_resnet(self, roots: torch.Tensor, active: torch.Tensor | None, cpuct: float, nsims: int, model):

@@ -75,6 +75,9 @@ _SIGS = {
     "bk_stem_tower_u_floats": (_i, []),
     "bk_resnet_stem_tower_heads": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
+    "bk_leafnet_x3_weight_bytes": (_i, [_i]),
+    "bk_leafnet_x3_supported": (_i, [_i]),
+    "bk_leafnet_x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp] + [_vp] * 8 + [_i, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

@@ -266,6 +266,70 @@ def pack_stem_tower(w: torch.Tensor) -> torch.Tensor:
     return w.float()[16 * kb + (lane & 15), 4 * (st % 2) + (lane >> 4), t // 3, t % 3].contiguous().view(-1)
 
 
+def pack_x3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """[64, cin, 3, 3] conv weights (cin 8: the stem, 64: a tower conv) -> bk_leafnet_x3's operands:
+    (split weights as uint8 bytes, inverse scales f32 [64]).
+
+    GEMM view: A[o][k] with k = tap * cin + c (tap = 3 ky + kx), K padded to 32-wide chunks (the
+    stem's 72 -> 96 with zeros). Row o is scaled by 2^e_o so that its largest magnitude lies in
+    [2^14, 2^15), then split hi = f16(x), lo = f16(x - hi); inverse scale 2^-e_o. Fragment order:
+    [chunk][wave 4][part hi/lo][lane 64][8 f16], lane l of wave w holding row 16w + l%16, columns
+    32 chunk + 8 (l/16) .. +7 (the A operand of v_mfma_f32_16x16x32_f16)."""
+    cout, cin = w.shape[0], w.shape[1]
+    assert cout == 64 and w.shape[2:] == (3, 3) and cin in (8, 64)
+    a = w.detach().to("cpu", torch.float64).permute(0, 2, 3, 1).reshape(64, 9 * cin)  # k = tap * cin + c
+    K = (a.shape[1] + 31) // 32 * 32
+    a = torch.cat([a, a.new_zeros(64, K - a.shape[1])], dim=1)
+    mx = a.abs().amax(dim=1)
+    _, e = torch.frexp(mx)
+    e = torch.where(mx > 0, 15 - e, torch.zeros_like(e)).to(torch.float64)
+    scaled = a * torch.pow(2.0, e).view(64, 1)
+    hi = scaled.to(torch.float16)
+    lo = (scaled - hi.to(torch.float64)).to(torch.float16)
+    parts = torch.stack([hi, lo])                                   # [2][64][K]
+    parts = parts.view(2, 4, 16, K // 32, 4, 8)                     # [part][wave][row][chunk][k-group][8]
+    packed = parts.permute(3, 1, 0, 4, 2, 5).contiguous()           # [chunk][wave][part][k-group][row][8]
+    inv = torch.pow(2.0, -e).to(torch.float32)
+    return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous()
+
+
+def net_math() -> str:
+    """The leaf ResNet's arithmetic on the device: "x3" (default) = bk_leafnet_x3, split-f16 MFMA
+    products with f32 accumulation (fp32-class accuracy, tests/test_leafnet_gpu.py); "f32" =
+    the round-1 kernels on the f32 MFMA (BK_NET_MATH=f32)."""
+    import os
+
+    m = os.environ.get("BK_NET_MATH", "x3")
+    if m not in ("x3", "f32"):
+        raise ValueError(f"BK_NET_MATH must be x3 or f32, got {m!r}")
+    return m
+
+
+def leafnet_x3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
+    """bk_leafnet_x3: the planar observation [B, 8, N, N] -> (policy features [B, 2*N*N], values
+    [B, P][, tower output [B, 64, N, N] channels_last]) in one launch."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, cin, N, _ = obs.shape
+    assert cin == 8 and obs.dtype == torch.float32 and obs.is_contiguous()
+    f = model.f
+    lib = load_library()
+    nl = 2 * len(f.blocks)
+    assert model.x3_wtower.numel() == nl * lib.bk_leafnet_x3_weight_bytes(64)
+    assert model.x3_wstem.numel() == lib.bk_leafnet_x3_weight_bytes(8)
+    P = f.value_fc2.out_features
+    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=obs.device)
+    v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
+    out = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device,
+                      memory_format=torch.channels_last) if want_out else None
+    h = model.x3_heads
+    _check(lib.bk_leafnet_x3(
+        ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
+        _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), *[_ptr(t) for t in h[1:]], P, _ptr(pf),
+        _ptr(v), None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
+    return (pf, v, out) if want_out else (pf, v)
+
+
 def tower_enabled() -> bool:
     """BK_TOWER=0 runs the residual tower as one bk_conv3x3 launch per layer instead of the fused
     bk_resnet_tower (same arithmetic; for comparisons)."""
@@ -381,6 +445,7 @@ class LeafResNet(nn.Module):
         self.features = features  # return (policy features [B, 2*N*N], v): the search applies policy_out
         f = self.f
         self.native = f.stem.out_channels == 64 and f.stem.in_channels in (4, 8)
+        self.x3 = False
         if self.native:
             self.register_buffer("w_stem", pack_conv3x3(f.stem.weight.detach()))
             for i, (c1, c2) in enumerate(f.blocks):
@@ -392,6 +457,18 @@ class LeafResNet(nn.Module):
                 convs = [c for blk in f.blocks for c in blk]
                 self.register_buffer("u_tower", pack_tower([c.weight.detach() for c in convs]))
                 self.register_buffer("b_tower", torch.cat([c.bias.detach().float() for c in convs]).contiguous())
+            self.x3 = f.stem.in_channels == 8 and len(f.blocks) > 0
+            if self.x3:  # bk_leafnet_x3's operands: split f16 weights + inverse scales
+                ws, ss = pack_x3(f.stem.weight)
+                self.register_buffer("x3_wstem", ws)
+                self.register_buffer("x3_sstem", ss)
+                packs = [pack_x3(c.weight) for c in convs]
+                self.register_buffer("x3_wtower", torch.cat([p[0] for p in packs]).contiguous())
+                self.register_buffer("x3_stower", torch.cat([p[1] for p in packs]).contiguous())
+                c = lambda t: t.detach().float().contiguous()  # noqa: E731
+                self.x3_heads = [c(f.stem.bias), c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias),
+                                 c(f.value_conv.weight.view(64)), c(f.value_conv.bias), f.value_fc1_wt(),
+                                 c(f.value_fc1.bias), c(f.value_fc2.weight), c(f.value_fc2.bias)]
 
     @torch.no_grad()
     def forward(self, x):
@@ -401,6 +478,13 @@ class LeafResNet(nn.Module):
             # planar observation in (as the search writes it), NHWC activations through the tower
             from .engine import load_library
 
+            if self.x3 and net_math() == "x3" and load_library().bk_leafnet_x3_supported(x.shape[2]):
+                # the whole net in one launch on split-f16 MFMA products (bk_leafnet_x3)
+                pf, v = leafnet_x3(x.float().contiguous(), self)
+                if self.features:
+                    return pf, v
+                logits = f.policy_out(pf)
+                return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
             fused = n and tower_enabled() and load_library().bk_tower_supported(x.shape[2])
             if fused and f.stem.in_channels == 8:
                 # stem conv, tower and heads in one launch (bk_resnet_stem_tower_heads)

@@ -311,6 +311,24 @@ int bk_resnet_stem_tower_heads(const float* obs, int B, int N, int cin, const fl
                                const float* w1t, const float* b1, const float* w2, const float* b2, int P, float* pf,
                                float* vout, void* stream);
 
+/* The whole leaf ResNet body (models/blokus_nnet.py:135-150, eval-mode BN folded; the net the
+ * reference's BlokusNNetWrapper.predict runs per leaf, neural_network.py:92-110) in one launch,
+ * one workgroup per board, on the f16 matrix cores with fp32-class accuracy: every fp32 operand
+ * is scaled by a power of two and split into two f16 halves, products taken as hi*hi + lo*hi +
+ * hi*lo with f32 accumulation (leafnet.hip). obs [B][8][N][N] f32 (planar observation) -> policy
+ * features pf [B][2NN] (relu(policy 1x1 conv), channel-major) and values vout [B][P]
+ * (tanh(value MLP)); out (may be NULL): the tower output [B][N][N][64] f32. wstem / wtower:
+ * split weights in the kernel's fragment order (nets.py pack_x3; bk_leafnet_x3_weight_bytes(8)
+ * and nlayers x bk_leafnet_x3_weight_bytes(64) bytes), sstem [64] / stower [nlayers][64] the
+ * inverse weight scales, bstem [64] / btower [nlayers][64] the biases; head weights as
+ * bk_resnet_heads. N = 14 or 20 (bk_leafnet_x3_supported), cin = 8, nlayers >= 1. */
+int bk_leafnet_x3_weight_bytes(int cin);
+int bk_leafnet_x3_supported(int N);
+int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
+                  int nlayers, const void* wtower, const float* stower, const float* btower, const float* wp,
+                  const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
+                  const float* w2, const float* b2, int P, float* pf, float* vout, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

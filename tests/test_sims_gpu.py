@@ -17,8 +17,10 @@ def _leaf_model(eng, blocks=2, seed=0):
 
 
 @pytest.mark.parametrize("N,T,sims", [(20, 12, 9), (20, 5, 3), (14, 7, 6)])
-def test_fused_simulations_match_stagewise(N, T, sims):
-    """k_sims<20> and k_sims<14> (the two board sizes the fused tower supports)."""
+def test_fused_simulations_match_stagewise(N, T, sims, monkeypatch):
+    """k_sims<20> and k_sims<14> (the two board sizes the fused tower supports), against the
+    staged launches with the same (f32) net."""
+    monkeypatch.setenv("BK_NET_MATH", "f32")
     from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
     from blokus_rl_amd.boards import random_boards
     from blokus_rl_amd.engine import Engine
@@ -58,6 +60,8 @@ def test_selfplay_plies_match_eager(monkeypatch, fused, graph):
     from blokus_rl_amd.nets import ResNet
 
     eng = Engine(20, 4, 5)
+
+    monkeypatch.setenv("BK_NET_MATH", "f32" if fused == "1" else "x3")
 
     def run(f, g):
         monkeypatch.setenv("BK_SIM_FUSED", f)
