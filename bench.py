@@ -414,7 +414,7 @@ def main():
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
         kname = out["roofline"].get("kernel", "").split(" ")[0]
-        if kname.startswith("k_conv3x3") or kname.startswith("k_tower"):
+        if kname.startswith("k_conv3x3") or kname.startswith("k_tower") or kname.startswith("k_leafnet"):
             # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)
             out["roofline"]["traffic"] = _pmc_traffic(kname, args.games)
         if args.workload == "all":

@@ -131,7 +131,7 @@ def time_leaf_conv(sp, reps: int = 5):
     st = torch.cuda.current_stream(sp.eng.device)
     events = []
     orig_conv, orig_tower, orig_th = nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads
-    orig_sth = nets.resnet_stem_tower_heads
+    orig_sth, orig_x3 = nets.resnet_stem_tower_heads, nets.leafnet_x3
 
     def timed(fn):
         def run(*a, **k):
@@ -141,12 +141,12 @@ def time_leaf_conv(sp, reps: int = 5):
             e0.record(st)
             y = fn(*a, **k)
             e1.record(st)
-            events.append((e0, e1, fn is not orig_conv, fn is orig_sth))
+            events.append((e0, e1, fn is not orig_conv, fn is orig_sth or fn is orig_x3, fn is orig_x3))
             return y
         return run
 
     nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads = timed(orig_conv), timed(orig_tower), timed(orig_th)
-    nets.resnet_stem_tower_heads = timed(orig_sth)
+    nets.resnet_stem_tower_heads, nets.leafnet_x3 = timed(orig_sth), timed(orig_x3)
     try:
         model(obs)  # warm
         events.clear()
@@ -154,15 +154,26 @@ def time_leaf_conv(sp, reps: int = 5):
             model(obs)
     finally:
         nets.conv3x3, nets.resnet_tower, nets.resnet_tower_heads = orig_conv, orig_tower, orig_th
-        nets.resnet_stem_tower_heads = orig_sth
+        nets.resnet_stem_tower_heads, nets.leafnet_x3 = orig_sth, orig_x3
     torch.cuda.synchronize()
     if not events:
         return None
-    fused, with_stem = events[0][2], events[0][3]
+    fused, with_stem, x3 = events[0][2], events[0][3], events[0][4]
     ms = sum(ev[0].elapsed_time(ev[1]) for ev in events) / len(events)
     layers = nconv if fused else 1
     stem = 2.0 * G * N * N * 64 * 9 * model.f.stem.in_channels if with_stem else 0.0
     direct = 2.0 * G * N * N * 64 * 9 * 64 * layers + stem
+    if x3:
+        # k_leafnet_x3: per board, layer and 16-pixel group, 3 f16 MFMAs 16x16x32 per K chunk of 32 in
+        # each of the 4 waves (K = 9*64 = 576: 18 chunks; the stem's 72 padded to 96: 3 chunks)
+        ng = (N * N + 15) // 16
+        per_mfma = 2.0 * 16 * 16 * 32
+        flop = G * 4 * ng * 3 * per_mfma * (18 * nconv + 3)
+        return {"ms": ms, "flop": flop, "direct": direct, "launches": 1, "peak": FP16_PEAK,
+                "kernel": "k_leafnet_x3 (the leaf ResNet in one launch, one workgroup per board: the stem and %d "
+                          "direct 3x3 convs 64->64 as f16 MFMA 16x16x32 on split operands, 3 products per fp32 "
+                          "product, f32 accumulation; bias/ReLU/residual, the heads' 1x1 convs and value MLP fused)"
+                          % nconv}
     if load_library().bk_conv3x3_form(N, 64) == 1:
         flop = 2.0 * 16 * 64 * 64 * G * (N // 2) ** 2 * layers + stem
         name = ("k_tower_wino (the leaf ResNet in one launch, one workgroup per board: %sthe residual tower of "
@@ -171,7 +182,17 @@ def time_leaf_conv(sp, reps: int = 5):
                 "k_conv3x3_wino2 (Winograd F(2x2,3x3), f32 MFMA, 64->64, fused bias+ReLU)")
     else:
         flop, name = direct, "k_conv3x3 (direct, f32 MFMA, 64->64, fused bias+ReLU)"
-    return {"ms": ms, "flop": flop, "kernel": name, "direct": direct, "launches": 1 if fused else nconv}
+    return {"ms": ms, "flop": flop, "kernel": name, "direct": direct, "launches": 1 if fused else nconv,
+            "peak": FP32_PEAK}
+
+
+def net_dtype(args) -> str:
+    from ..nets import net_math
+
+    if args.nn_dtype == "fp32" and args.model == "resnet" and net_math() == "x3":
+        return ("fp32 net (fp32 operands split into f16 hi+lo, 3 f16 MFMA products, f32 accumulation: fp32-class "
+                "error, tests/test_leafnet_gpu.py) / f64 search / u32 bitboards")
+    return f"{args.nn_dtype} net / f64 search / u32 bitboards"
 
 
 def bench_selfplay(args, world, rank):
@@ -205,7 +226,7 @@ def bench_selfplay(args, world, rank):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": f"{args.nn_dtype} net / f64 search / u32 bitboards",
+        "dtype": net_dtype(args),
         "data": "synthetic: continuous self-play from the empty board, random-init ResNet weights (seed 0)",
         "config": {"workload": "config 3 (N=1) / 4 (N=8): AlphaZero self-play 20x20, 256 concurrent games per GPU, "
                                "100 sims/move, ResNet-5x64 leaf eval", "global_batch": G * world,
@@ -215,9 +236,9 @@ def bench_selfplay(args, world, rank):
                             "frac": achieved / HBM_PEAK, "traffic": None,
                             "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms},
         "net_roofline": {"bound": "mfma",
-                         "kernel": "leaf ResNet forward (stem k_conv3x3, k_tower_wino, k_resnet_heads, sparse policy "
-                                   "head); FLOP counted as the direct-convolution network (347.5 MFLOP/leaf), so "
-                                   "frac can exceed 1 with the Winograd tower",
+                         "kernel": "leaf ResNet forward (the leaf-net launch + the sparse policy head); FLOP counted "
+                                   "as the fp32 direct-convolution network (347.5 MFLOP/leaf) against the f32 MFMA "
+                                   "peak: the fp32-equivalent rate",
                          "achieved": net_flops / (ms.get("net", 1e9) * 1e-3) / 1e12 if ms else None,
                          "peak": net_peak / 1e12, "unit": "TFLOP/s",
                          "frac": (net_flops / (ms["net"] * 1e-3)) / net_peak if ms else None},
@@ -225,10 +246,10 @@ def bench_selfplay(args, world, rank):
         "engine_counters": delta,
     }
     if conv is not None:
-        cms, cflop, dflop = conv["ms"], conv["flop"], conv["direct"]
+        cms, cflop, dflop, cpeak = conv["ms"], conv["flop"], conv["direct"], conv["peak"]
         out["tower_roofline"] = {"bound": "mfma", "kernel": conv["kernel"],
-                           "achieved": cflop / (cms * 1e-3) / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s",
-                           "frac": cflop / (cms * 1e-3) / FP32_PEAK, "traffic": None, "kernel_ms": cms,
+                           "achieved": cflop / (cms * 1e-3) / 1e12, "peak": cpeak / 1e12, "unit": "TFLOP/s",
+                           "frac": cflop / (cms * 1e-3) / cpeak, "traffic": None, "kernel_ms": cms,
                            "flop_per_launch": cflop, "units_per_launch": G,
                            "direct_conv_equiv_tflops": dflop / (cms * 1e-3) / 1e12,
                            "launches_per_sim_step": conv["launches"],

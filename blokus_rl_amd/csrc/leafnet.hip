@@ -15,9 +15,10 @@
 // Convolutions are direct (implicit GEMM): M = 16 output channels per wave (4 waves = 64), N = 16
 // pixels per group (NG = ceil(N*N/16) groups cover the board), K = 9 taps x Cin in chunks of 32
 // (tap t = c/2, channel half c%2 for Cin = 64; taps 4c..4c+3 x 8 channels for the stem). The
-// board's layer input lives in LDS as a zero-haloed (N+2)^2 pixel grid of split halves
-// (kPixBytes per pixel: hi[64] | lo[64] | pad): the B fragment of lane l is one ds_read_b128 per
-// half at pixel (16g + l%16) shifted by the tap, channels 8(l/16).. of the chunk. The A fragments
+// board's layer input lives in LDS as zero-haloed pixel grids of split halves, one plane per
+// 8 channels (ln_plane): the B fragment of lane l is one ds_read_b128 per half at the slot of
+// column l%16 of group g (LnPixMap) shifted by the tap, in the plane of channels 8(l/16).. of
+// the chunk. The A fragments
 // (weights) stream from global memory (L2-resident across the 32 boards of an XCD), one chunk
 // ahead. The accumulators of all NG groups stay in registers for the layer; the epilogue applies
 // scale, bias, (residual), ReLU, finds the board maximum, splits and writes the next layer input
@@ -36,16 +37,77 @@ using f32x2 = float __attribute__((ext_vector_type(2)));
 using u32x4 = unsigned __attribute__((ext_vector_type(4)));
 using u32x2 = unsigned __attribute__((ext_vector_type(2)));
 
+#ifndef BK_LN_STAMP
+#define BK_LN_STAMP 0  // timing diagnostics only: per-wave s_memtime stamps (bk_ln_stamps)
+#endif
+#if BK_LN_STAMP
+constexpr int kLnStamps = 32;
+__device__ unsigned long long g_ln_stamps[256 * 4 * kLnStamps];
+#define LNSTAMP(i, v)                                                                                          \
+  do {                                                                                                         \
+    if (l == 0 && blockIdx.x < 256) g_ln_stamps[(blockIdx.x * 4 + wave) * kLnStamps + (i)] = (v);              \
+  } while (0)
+#else
+#define LNSTAMP(i, v) \
+  do {                \
+  } while (0)
+#endif
+
 constexpr int kLnThreads = 256;
-constexpr int kPixBytes = 272;     // hi[64] f16 | lo[64] f16 | 16 B (pixel stride = 17 x 16 B: spreads banks)
-constexpr int kStemPixBytes = 32;  // hi[8] f16 | lo[8] f16
 constexpr int kStemCinX3 = 8;
 constexpr int kBlock = 64 * 8;     // f16 per (chunk, wave, part) block of packed weights: 64 lanes x 8
 
 __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3; }
 
-// LDS bytes of k_leafnet_x3<N>: the activation grid, the stem's input grid, 4 wave maxima
-__host__ __device__ constexpr int ln_lds_bytes(int N) { return (N + 2) * (N + 2) * (kPixBytes + kStemPixBytes) + 64; }
+// The layer input in LDS: 16 planes (hi halves of channels 8q..8q+7 in plane q, lo halves in
+// plane 8 + q), each a zero-haloed grid of (N+2) rows x ln_row(N) slots of 16 B (8 f16). A plane
+// is a multiple of 256 B (the LDS bank period), so the 16-B chunk of every plane of a slot sits in
+// the same 4 banks, and the lanes of one ds_read_b128 lane group (16 distinct pixels of a group,
+// k-groups ks and ks^1) are conflict-free when their slots differ mod 16 (LnPixMap). The stem's
+// input (8 channels) takes two more planes (hi, lo).
+__host__ __device__ constexpr int ln_row(int N) { return N == 14 ? 18 : N + 2; }  // slot classes mod 16 balanced
+__host__ __device__ constexpr int ln_plane(int N) { return ((N + 2) * ln_row(N) * 16 + 255) / 256 * 256; }
+// LDS bytes of k_leafnet_x3<N>: 16 activation planes, 2 stem planes, wave maxima (2 x 4 + 4)
+__host__ __device__ constexpr int ln_lds_bytes(int N) { return 18 * ln_plane(N) + 64; }
+
+// The board's pixels in MFMA columns: slot (g, n) of pixel group g, column n. Any bijection works
+// (reads and writes use the same map); this one gives each group 16 pixels whose grid slots are
+// distinct mod 16 where the slot classes allow (one pixel per class, leftovers fill the gaps),
+// so the B-fragment reads are bank-conflict-free. Entries: grid slot (row + 1) * ln_row + col + 1,
+// or -1 for a spare column (N*N not a multiple of 16).
+template <int N>
+struct LnPixMap {
+  static constexpr int NN = N * N, NG = (NN + 15) / 16, RS = ln_row(N);
+  int slot[NG * 16];
+  constexpr LnPixMap() : slot() {
+    bool used[NN] = {};
+    for (int i = 0; i < NG * 16; ++i) slot[i] = -1;
+    for (int g = 0; g < NG; ++g)
+      for (int r = 0; r < 16; ++r)
+        for (int p = 0; p < NN; ++p) {
+          const int sl = (p / N + 1) * RS + p % N + 1;
+          if (!used[p] && sl % 16 == r) {
+            used[p] = true;
+            slot[g * 16 + r] = sl;
+            break;
+          }
+        }
+    int p = 0;
+    for (int i = 0; i < NG * 16; ++i) {
+      if (slot[i] >= 0) continue;
+      while (p < NN && used[p]) ++p;
+      if (p == NN) break;
+      used[p] = true;
+      slot[i] = (p / N + 1) * RS + p % N + 1;
+    }
+  }
+};
+template <int N>
+__device__ constexpr LnPixMap<N> kLnPixMap{};
+template <int N>
+__device__ __forceinline__ int ln_pixel(int slot) {  // grid slot -> board pixel index
+  return (slot / ln_row(N) - 1) * N + slot % ln_row(N) - 1;
+}
 
 __device__ __forceinline__ f32x4 mfma16(h16x8 a, h16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -58,6 +120,22 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigne
   const f32x2 r = f32x2{x0, x1} - hf;
   hi = __builtin_bit_cast(unsigned, h);
   lo = __builtin_bit_cast(unsigned, __builtin_convertvector(r, h16x2));
+}
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 // the power of two that brings the largest magnitude m into [2^14, 2^15)
@@ -78,15 +156,16 @@ __device__ __forceinline__ float block_max(float m, float* red, int wave, int l)
 }
 
 // One K chunk over the board's NG pixel groups: per group the B fragments (hi, lo) from the grid
-// (LDS; read two groups ahead) and acc[g] += ah*bh + al*bh + ah*bl. The MFMAs are inline asm with
+// (LDS; read two groups ahead; pb[g] = the lane's slot in bytes, coff = the chunk's plane and tap
+// offset) and acc[g] += ah*bh + al*bh + ah*bl. The MFMAs are inline asm with
 // the accumulator in place in AGPRs (srcC = vdst: back-to-back accumulation, no copies); INIT
 // starts the accumulators from 0. HALF: byte offset of the lo halves from the hi halves.
-template <int NG, bool INIT, int PIX, int HALF>
+template <int NG, bool INIT, int HALF>
 __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, const unsigned char* grid,
-                                         const int (&pp)[NG], int coff) {
+                                         const int (&pb)[NG], int coff) {
   h16x8 rb[3][2];
   auto load = [&](int g, int slot) {
-    const unsigned char* q = grid + pp[g] * PIX + coff;
+    const unsigned char* q = grid + pb[g] + coff;
     rb[slot][0] = *reinterpret_cast<const h16x8*>(q);
     rb[slot][1] = *reinterpret_cast<const h16x8*>(q + HALF);
   };
@@ -131,29 +210,35 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
                                                               const float* __restrict__ bstem,
                                                               const h16x8* __restrict__ wt,
                                                               const float* __restrict__ st,
-                                                              const float* __restrict__ bt, int nlayers,
+                                                              const float* __restrict__ bt,
+                                                              const float* __restrict__ bounds, int nlayers,
                                                               LnHeads hd, float* __restrict__ xout) {
-  constexpr int NN = N * N, NP = N + 2, NG = (NN + 15) / 16, PIX_IT = (NN + kLnThreads - 1) / kLnThreads;
+  constexpr int NN = N * N, RS = ln_row(N), NG = (NN + 15) / 16, PIX_IT = (NN + kLnThreads - 1) / kLnThreads;
+  constexpr int PL = ln_plane(N);
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  unsigned char* act = lds;                                 // [NP*NP][kPixBytes]
-  unsigned char* sin = lds + NP * NP * kPixBytes;           // [NP*NP][kStemPixBytes]
-  float* red = reinterpret_cast<float*>(sin + NP * NP * kStemPixBytes);
+  unsigned char* act = lds;                  // 16 planes [hi q | lo q][(N+2) x RS slots][16 B]
+  unsigned char* sin = lds + 16 * PL;        // 2 planes: the stem input hi, lo
+  float* red = reinterpret_cast<float*>(lds + 18 * PL);
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, n = l & 15, ks = l >> 4;
   const int oc = 16 * wave + 4 * ks;  // the lane's 4 output channels oc..oc+3 in the D fragments
   const size_t b = blockIdx.x;
+  LNSTAMP(0, __builtin_amdgcn_s_memtime());
+  LNSTAMP(30, __builtin_amdgcn_s_memrealtime());
 
   // zero both grids (the halo stays zero; interiors are overwritten before they are read)
-  for (int i = tid; i < NP * NP * (kPixBytes + kStemPixBytes) / 16; i += kLnThreads)
-    reinterpret_cast<u32x4*>(lds)[i] = u32x4{0u, 0u, 0u, 0u};
+  for (int i = tid; i < 18 * PL / 16; i += kLnThreads) reinterpret_cast<u32x4*>(lds)[i] = u32x4{0u, 0u, 0u, 0u};
 
-  // the lane's pixel of each group (clamped to the board for the last group's spare lanes) as a
-  // padded-grid index
-  int pp[NG];
+  // the lane's grid slot in each group, in bytes (a spare column reads slot 0 of the halo: zeros),
+  // and the mask of groups where the lane's column is a board pixel
+  int pb[NG];
+  unsigned valid = 0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    const int p = 16 * g + n < NN ? 16 * g + n : NN - 1;
-    pp[g] = (p / N + 1) * NP + p % N + 1;
+    const int sl = kLnPixMap<N>.slot[16 * g + n];
+    pb[g] = (sl >= 0 ? sl : 0) * 16;
+    valid |= (sl >= 0 ? 1u : 0u) << g;
   }
+  auto is_valid = [&](int g) { return NN % 16 == 0 || ((valid >> g) & 1u); };
 
   // ---- stem input: the planar observation [8][N][N] of the board, scaled by its maximum, split
   const float* ob = obs + b * kStemCinX3 * NN;
@@ -168,7 +253,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       m = fmaxf(m, fabsf(xin[it][c]));
     }
   }
-  int ex = scale_exp(block_max(m, red, wave, l));  // the barrier also orders the zeroing before the writes
+  const float max_obs = block_max(m, red + 8, wave, l);  // the barrier also orders the zeroing before the writes
+  int ex = scale_exp(max_obs);
 #pragma unroll
   for (int it = 0; it < PIX_IT; ++it) {
     const int p = tid + it * kLnThreads;
@@ -177,76 +263,125 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 #pragma unroll
       for (int q = 0; q < 4; ++q) split2(ldexpf(xin[it][2 * q], ex), ldexpf(xin[it][2 * q + 1], ex), h[q], o[q]);
       const u32x4 hi{h[0], h[1], h[2], h[3]}, lo{o[0], o[1], o[2], o[3]};
-      unsigned char* dst = sin + ((p / N + 1) * NP + p % N + 1) * kStemPixBytes;
+      unsigned char* dst = sin + ((p / N + 1) * RS + p % N + 1) * 16;
       *reinterpret_cast<u32x4*>(dst) = hi;
-      *reinterpret_cast<u32x4*>(dst + 16) = lo;
+      *reinterpret_cast<u32x4*>(dst + PL) = lo;
     }
   }
   __syncthreads();
+  LNSTAMP(1, __builtin_amdgcn_s_memtime());
 
   // ---- stem conv: 3 chunks; lane k-group ks of chunk j is tap 4j + ks (taps > 8 carry zero weights)
   f32x4 acc[NG];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int t = 4 * j + ks < 9 ? 4 * j + ks : 8;
-    const int toff = ((t / 3 - 1) * NP + (t % 3 - 1)) * kStemPixBytes;
+    const int toff = ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
     const h16x8 ah = wstem[((j * 4 + wave) * 2) * 64 + l], al = wstem[((j * 4 + wave) * 2 + 1) * 64 + l];
     if (j == 0)
-      ln_chunk<NG, true, kStemPixBytes, 16>(acc, ah, al, sin, pp, toff);
+      ln_chunk<NG, true, PL>(acc, ah, al, sin, pb, toff);
     else
-      ln_chunk<NG, false, kStemPixBytes, 16>(acc, ah, al, sin, pp, toff);
+      ln_chunk<NG, false, PL>(acc, ah, al, sin, pb, toff);
   }
   ln_mfma_drain();
+  LNSTAMP(2, __builtin_amdgcn_s_memtime());
 
-  // epilogue of a conv: y = acc * s + bias (+ x0) (ReLU) in place; returns the lane's max |y|
-  // over real pixels
-  auto epilogue = [&](const float* sv, const float* bv, bool relu, bool residual, const f32x4 (&x0)[NG]) {
-    float s[4], bb[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      s[r] = ldexpf(sv[oc + r], -ex);
-      bb[r] = bv[oc + r];
-    }
+  // Epilogue of a conv: y = acc * s + bias (+ x0) (ReLU), s = the inverse weight scale x 2^-ex_in.
+  // OUT: y is the next layer's input: scaled by 2^ex_out (ex_out from a bound on |y|, so no board
+  // reduction is needed before the split), split, and the packed halves kept in acc's registers
+  // until every wave has finished reading the grid (bar 1), then written; the lane's max |y|
+  // (unscaled) is returned for the next layer's bound. !OUT (the last conv): y stays in acc.
+  auto epilogue = [&](const float* sv, const float* bv, bool relu, bool residual, const f32x4 (&x0)[NG],
+                      bool out, int ex_out) {
+    f32x2 s01, s23, b01, b23;
+    s01.x = ldexpf(sv[oc], -ex);
+    s01.y = ldexpf(sv[oc + 1], -ex);
+    s23.x = ldexpf(sv[oc + 2], -ex);
+    s23.y = ldexpf(sv[oc + 3], -ex);
+    b01 = f32x2{bv[oc], bv[oc + 1]};
+    b23 = f32x2{bv[oc + 2], bv[oc + 3]};
+    const float up = ldexpf(1.0f, ex_out);
+    const f32x2 up2{up, up};
     const float floor = relu ? 0.0f : -__builtin_inff();
     float mx = 0.0f;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float y = fmaf(acc[g][r], s[r], bb[r]);
-        if (residual) y += x0[g][r];
-        y = fmaxf(y, floor);
-        acc[g][r] = y;
-        if (16 * g + n < NN) mx = fmaxf(mx, fabsf(y));
+      f32x2 y01 = pk_fma(f32x2{acc[g][0], acc[g][1]}, s01, b01);
+      f32x2 y23 = pk_fma(f32x2{acc[g][2], acc[g][3]}, s23, b23);
+      if (residual) {
+        y01 = pk_add(y01, f32x2{x0[g][0], x0[g][1]});
+        y23 = pk_add(y23, f32x2{x0[g][2], x0[g][3]});
+      }
+      y01 = f32x2{fmaxf(y01.x, floor), fmaxf(y01.y, floor)};
+      y23 = f32x2{fmaxf(y23.x, floor), fmaxf(y23.y, floor)};
+      if (is_valid(g)) mx = fmaxf(fmaxf(mx, fmaxf(fabsf(y01.x), fabsf(y01.y))), fmaxf(fabsf(y23.x), fabsf(y23.y)));
+      if (out) {
+        const f32x2 z01 = pk_mul(y01, up2), z23 = pk_mul(y23, up2);
+        unsigned h0, h1, l0, l1;
+        split2(z01.x, z01.y, h0, l0);
+        split2(z23.x, z23.y, h1, l1);
+        acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
+                       __builtin_bit_cast(float, l1)};
+      } else {
+        acc[g] = f32x4{y01.x, y01.y, y23.x, y23.y};
       }
     }
     return mx;
   };
-  // the layer output (acc) scaled by 2^ex and split into the activation grid (after a barrier:
-  // every wave has finished reading the grid)
+  // the packed halves in acc -> the activation grid (channels oc..oc+3: plane oc/8 = 2 wave + ks/2,
+  // bytes 8 (ks & 1) of the slot)
   auto write_act = [&]() {
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if (16 * g + n < NN) {
-        unsigned h0, h1, l0, l1;
-        split2(ldexpf(acc[g][0], ex), ldexpf(acc[g][1], ex), h0, l0);
-        split2(ldexpf(acc[g][2], ex), ldexpf(acc[g][3], ex), h1, l1);
-        unsigned char* dst = act + pp[g] * kPixBytes + 2 * oc;
-        *reinterpret_cast<u32x2*>(dst) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2*>(dst + 128) = u32x2{l0, l1};
+      if (is_valid(g)) {
+        unsigned char* dst = act + (2 * wave + (ks >> 1)) * PL + pb[g] + 8 * (ks & 1);
+        // bit_cast the whole vector: hipcc's __builtin_bit_cast of an ext_vector element reads
+        // element 0 whatever the index (ROCm 7.2)
+        const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);
+        *reinterpret_cast<u32x2*>(dst) = u32x2{w.x, w.y};
+        *reinterpret_cast<u32x2*>(dst + 8 * PL) = u32x2{w.z, w.w};
       }
     }
   };
+  // the scale of a conv's output from the bound |y| <= A max_in + B (A = the largest row L1 norm
+  // of the weights, B = the largest |bias|: nets.pack_x3)
+  auto out_exp = [&](int conv, float max_in) { return scale_exp(bounds[2 * conv] * max_in + bounds[2 * conv + 1]); };
+  // wave maxima -> red[par][wave] before the barrier, the board maximum after it
+  auto post_max = [&](float mx, int par) {
+    mx = wave_max_f(mx);
+    if (l == 0) red[4 * par + wave] = mx;
+  };
+  auto board_max = [&](int par) {
+    return fmaxf(fmaxf(red[4 * par], red[4 * par + 1]), fmaxf(red[4 * par + 2], red[4 * par + 3]));
+  };
 
   f32x4 x0[NG];
+  float max_in;
   {
-    const float mx = epilogue(sstem, bstem, true, false, x0);
+    const int ex_out = out_exp(0, max_obs);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) x0[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the stem output itself is kept (unscaled) for the tower's final residual
+    const float mx = epilogue(sstem, bstem, true, false, x0, false, 0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) x0[g] = acc[g];
-    ex = scale_exp(block_max(mx, red, wave, l));
+    const float up = ldexpf(1.0f, ex_out);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      unsigned h0, h1, l0, l1;
+      split2(x0[g][0] * up, x0[g][1] * up, h0, l0);
+      split2(x0[g][2] * up, x0[g][3] * up, h1, l1);
+      acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
+                     __builtin_bit_cast(float, l1)};
+    }
+    post_max(mx, 0);
+    __syncthreads();  // the stem's input planes are a separate region: nothing else to wait for
     write_act();
     __syncthreads();
+    max_in = board_max(0);
+    ex = ex_out;
   }
+  LNSTAMP(3, __builtin_amdgcn_s_memtime());
 
   // ---- residual tower: nlayers convs 64 -> 64; ReLU after each block's first conv; the last
   // adds x0 and takes the ReLU (x = relu(x + res_blocks(x)), blokus_nnet.py:140-141)
@@ -256,11 +391,11 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     h16x8 ah = wl[0], al = wl[64];
     auto coff_of = [&](int c) {
       const int t = c >> 1;
-      return ((t / 3 - 1) * NP + (t % 3 - 1)) * kPixBytes + (c & 1) * 64 + ks * 16;
+      return (4 * (c & 1) + ks) * PL + ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
     };
     {
       const h16x8 nh = wl[8 * 64], nl = wl[8 * 64 + 64];
-      ln_chunk<NG, true, kPixBytes, 128>(acc, ah, al, act, pp, coff_of(0));
+      ln_chunk<NG, true, 8 * PL>(acc, ah, al, act, pb, coff_of(0));
       ah = nh;
       al = nl;
     }
@@ -270,26 +405,34 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         nh = wl[(c + 1) * 8 * 64];
         nl = wl[(c + 1) * 8 * 64 + 64];
       }
-      ln_chunk<NG, false, kPixBytes, 128>(acc, ah, al, act, pp, coff_of(c));
+      ln_chunk<NG, false, 8 * PL>(acc, ah, al, act, pb, coff_of(c));
       ah = nh;
       al = nl;
     }
     ln_mfma_drain();
+    if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
     const bool last = layer + 1 == nlayers;
-    const float mx = epilogue(st + layer * 64, bt + layer * 64, last || !(layer & 1), last, x0);
     if (!last) {
-      ex = scale_exp(block_max(mx, red, wave, l));
+      const int ex_out = out_exp(layer + 1, max_in);
+      const float mx = epilogue(st + layer * 64, bt + layer * 64, !(layer & 1), false, x0, true, ex_out);
+      post_max(mx, (layer + 1) & 1);
+      __syncthreads();  // every wave has finished reading the grid
       write_act();
       __syncthreads();
+      max_in = board_max((layer + 1) & 1);
+      ex = ex_out;
+    } else {
+      epilogue(st + layer * 64, bt + layer * 64, true, true, x0, false, 0);
     }
+    if (layer < 8) LNSTAMP(5 + 2 * layer, __builtin_amdgcn_s_memtime());
   }
 
   // ---- outputs: the tower output (optional) and the heads (blokus_nnet.py:146-150, BN folded)
   if (xout) {
 #pragma unroll
     for (int g = 0; g < NG; ++g)
-      if (16 * g + n < NN)
-        *reinterpret_cast<f32x4*>(xout + (b * NN + 16 * g + n) * 64 + oc) = acc[g];
+      if (is_valid(g))
+        *reinterpret_cast<f32x4*>(xout + (b * NN + ln_pixel<N>(pb[g] / 16)) * 64 + oc) = acc[g];
   }
   __syncthreads();  // every wave is done with the activation grid: the heads' scratch reuses it
   float* hp = reinterpret_cast<float*>(act);  // [NN][4 waves][3]
@@ -309,8 +452,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         a += __shfl_xor(a, 32);
         d[k] = a;
       }
-      if (ks == 0 && 16 * g + n < NN) {
-        float* dst = hp + ((16 * g + n) * 4 + wave) * 3;
+      if (ks == 0 && is_valid(g)) {
+        float* dst = hp + (ln_pixel<N>(pb[g] / 16) * 4 + wave) * 3;
         dst[0] = d[0];
         dst[1] = d[1];
         dst[2] = d[2];
@@ -318,6 +461,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     }
   }
   __syncthreads();
+  LNSTAMP(20, __builtin_amdgcn_s_memtime());
   // pf = relu(policy 1x1 conv + bp) (channel-major), vfeat = relu(value 1x1 conv + bv), then
   // v = tanh(W2 relu(W1 vfeat + b1) + b2); the 4 waves sweep quarters of W1's inputs
   float* vfeat = hp + NN * 12;
@@ -356,6 +500,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       if (l == 0) hd.v[b * hd.P + q] = tanhf(sum + hd.b2[q]);
     }
   }
+  LNSTAMP(29, __builtin_amdgcn_s_memtime());
+  LNSTAMP(31, __builtin_amdgcn_s_memrealtime());
 }
 
 static_assert(ln_lds_bytes(20) <= 160 * 1024, "k_leafnet_x3<20>: LDS");
@@ -373,11 +519,22 @@ int bk_leafnet_x3_weight_bytes(int cin) {
 
 int bk_leafnet_x3_supported(int N) { return N == 14 || N == 20; }
 
+#if BK_LN_STAMP
+int bk_ln_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ln_stamps), sizeof(g_ln_stamps)) == hipSuccess ? 0 : -1;
+}
+int bk_ln_stamps_clear() {
+  static unsigned long long zeros[256 * 4 * kLnStamps];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ln_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
-                  int nlayers, const void* wtower, const float* stower, const float* btower, const float* wp,
+                  int nlayers, const void* wtower, const float* stower, const float* btower, const float* bounds,
+                  const float* wp,
                   const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
                   const float* w2, const float* b2, int P, float* pf, float* vout, float* out, void* stream) {
-  BK_REQUIRE(obs && wstem && sstem && bstem && wtower && stower && btower && B >= 0, "bad argument");
+  BK_REQUIRE(obs && wstem && sstem && bstem && wtower && stower && btower && bounds && B >= 0, "bad argument");
   BK_REQUIRE(wp && bp && wv && bv && w1t && b1 && w2 && b2 && pf && vout && P > 0, "bad argument");
   BK_REQUIRE(cin == kStemCinX3, "bk_leafnet_x3: the stem takes 8 observation planes");
   BK_REQUIRE(nlayers >= 1, "bk_leafnet_x3: at least one tower conv");
@@ -395,10 +552,10 @@ int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, co
   const h16x8* wt = reinterpret_cast<const h16x8*>(wtower);
   if (N == 20)
     hipLaunchKernelGGL(k_leafnet_x3<20>, dim3(B), dim3(kLnThreads), ln_lds_bytes(20), s, obs, ws, sstem, bstem, wt,
-                       stower, btower, nlayers, h, out);
+                       stower, btower, bounds, nlayers, h, out);
   else
     hipLaunchKernelGGL(k_leafnet_x3<14>, dim3(B), dim3(kLnThreads), ln_lds_bytes(14), s, obs, ws, sstem, bstem, wt,
-                       stower, btower, nlayers, h, out);
+                       stower, btower, bounds, nlayers, h, out);
   return launch_check("k_leafnet_x3");
 }
 

@@ -77,7 +77,7 @@ _SIGS = {
                                         _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "bk_leafnet_x3_weight_bytes": (_i, [_i]),
     "bk_leafnet_x3_supported": (_i, [_i]),
-    "bk_leafnet_x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp] + [_vp] * 8 + [_i, _vp, _vp, _vp, _vp]),
+    "bk_leafnet_x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8 + [_i, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

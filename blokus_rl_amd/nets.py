@@ -266,9 +266,11 @@ def pack_stem_tower(w: torch.Tensor) -> torch.Tensor:
     return w.float()[16 * kb + (lane & 15), 4 * (st % 2) + (lane >> 4), t // 3, t % 3].contiguous().view(-1)
 
 
-def pack_x3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-    """[64, cin, 3, 3] conv weights (cin 8: the stem, 64: a tower conv) -> bk_leafnet_x3's operands:
-    (split weights as uint8 bytes, inverse scales f32 [64]).
+def pack_x3(w: torch.Tensor, b: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """[64, cin, 3, 3] conv weights (cin 8: the stem, 64: a tower conv) and bias [64] ->
+    bk_leafnet_x3's operands: (split weights as uint8 bytes, inverse scales f32 [64], output bound
+    f32 [2] = (A, B) with |y| <= A max|x| + B for y = conv(x) + b: A the largest row L1 norm of
+    the weights, B the largest |bias|, both rounded up).
 
     GEMM view: A[o][k] with k = tap * cin + c (tap = 3 ky + kx), K padded to 32-wide chunks (the
     stem's 72 -> 96 with zeros). Row o is scaled by 2^e_o so that its largest magnitude lies in
@@ -290,7 +292,10 @@ def pack_x3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     parts = parts.view(2, 4, 16, K // 32, 4, 8)                     # [part][wave][row][chunk][k-group][8]
     packed = parts.permute(3, 1, 0, 4, 2, 5).contiguous()           # [chunk][wave][part][k-group][row][8]
     inv = torch.pow(2.0, -e).to(torch.float32)
-    return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous()
+    bmax = float(b.detach().abs().max()) if b is not None else 0.0
+    bound = torch.tensor([float(a.abs().sum(dim=1).max()) * (1 + 2 ** -16), bmax * (1 + 2 ** -16)],
+                         dtype=torch.float32)
+    return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous(), bound.to(w.device)
 
 
 def net_math() -> str:
@@ -325,7 +330,8 @@ def leafnet_x3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
     h = model.x3_heads
     _check(lib.bk_leafnet_x3(
         ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
-        _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), *[_ptr(t) for t in h[1:]], P, _ptr(pf),
+        _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), _ptr(model.x3_bounds),
+        *[_ptr(t) for t in h[1:]], P, _ptr(pf),
         _ptr(v), None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
     return (pf, v, out) if want_out else (pf, v)
 
@@ -459,12 +465,13 @@ class LeafResNet(nn.Module):
                 self.register_buffer("b_tower", torch.cat([c.bias.detach().float() for c in convs]).contiguous())
             self.x3 = f.stem.in_channels == 8 and len(f.blocks) > 0
             if self.x3:  # bk_leafnet_x3's operands: split f16 weights + inverse scales
-                ws, ss = pack_x3(f.stem.weight)
+                ws, ss, bs = pack_x3(f.stem.weight, f.stem.bias)
                 self.register_buffer("x3_wstem", ws)
                 self.register_buffer("x3_sstem", ss)
-                packs = [pack_x3(c.weight) for c in convs]
+                packs = [pack_x3(c.weight, c.bias) for c in convs]
                 self.register_buffer("x3_wtower", torch.cat([p[0] for p in packs]).contiguous())
                 self.register_buffer("x3_stower", torch.cat([p[1] for p in packs]).contiguous())
+                self.register_buffer("x3_bounds", torch.cat([bs] + [p[2] for p in packs]).contiguous())
                 c = lambda t: t.detach().float().contiguous()  # noqa: E731
                 self.x3_heads = [c(f.stem.bias), c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias),
                                  c(f.value_conv.weight.view(64)), c(f.value_conv.bias), f.value_fc1_wt(),

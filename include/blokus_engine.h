@@ -320,13 +320,14 @@ int bk_resnet_stem_tower_heads(const float* obs, int B, int N, int cin, const fl
  * (tanh(value MLP)); out (may be NULL): the tower output [B][N][N][64] f32. wstem / wtower:
  * split weights in the kernel's fragment order (nets.py pack_x3; bk_leafnet_x3_weight_bytes(8)
  * and nlayers x bk_leafnet_x3_weight_bytes(64) bytes), sstem [64] / stower [nlayers][64] the
- * inverse weight scales, bstem [64] / btower [nlayers][64] the biases; head weights as
- * bk_resnet_heads. N = 14 or 20 (bk_leafnet_x3_supported), cin = 8, nlayers >= 1. */
+ * inverse weight scales, bstem [64] / btower [nlayers][64] the biases, bounds [nlayers + 1][2]
+ * per conv (stem first) (A, B) with |conv(x) + b| <= A max|x| + B (the output scale); head weights
+ * as bk_resnet_heads. N = 14 or 20 (bk_leafnet_x3_supported), cin = 8, nlayers >= 1. */
 int bk_leafnet_x3_weight_bytes(int cin);
 int bk_leafnet_x3_supported(int N);
 int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
-                  int nlayers, const void* wtower, const float* stower, const float* btower, const float* wp,
-                  const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
+                  int nlayers, const void* wtower, const float* stower, const float* btower, const float* bounds,
+                  const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
                   const float* w2, const float* b2, int P, float* pf, float* vout, float* out, void* stream);
 
 #ifdef __cplusplus
