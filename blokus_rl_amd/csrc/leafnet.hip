@@ -59,6 +59,21 @@ constexpr int kBlock = 64 * 8;     // f16 per (chunk, wave, part) block of packe
 
 __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3; }
 
+// B-fragment pipeline: the grid reads of a group are issued kLnPf groups ahead of its MFMAs, in a
+// ring of kLnSlots register slots that runs on across chunk boundaries (the last kLnPf groups of
+// a chunk load the first kLnPf of the next), so the LDS latency is never exposed at a chunk start.
+// The slot of group g is g % kLnSlots in every chunk, which needs NG % kLnSlots == 0: the board's
+// groups are padded with spare ones (all columns spare: halo reads, no writes) up to a multiple.
+#ifndef BK_LN_PF
+#define BK_LN_PF 2  // groups of read-ahead (A/B knob, 1..4)
+#endif
+#ifndef BK_LN_WPF
+#define BK_LN_WPF 1  // chunks of weight read-ahead (A/B knob: 1 or 2)
+#endif
+constexpr int kLnPf = BK_LN_PF, kLnSlots = 5, kLnWpf = BK_LN_WPF;
+static_assert(kLnPf >= 1 && kLnPf < kLnSlots, "BK_LN_PF");
+__host__ __device__ constexpr int ln_groups(int N) { return ((N * N + 15) / 16 + kLnSlots - 1) / kLnSlots * kLnSlots; }
+
 // The layer input in LDS: 16 planes (hi halves of channels 8q..8q+7 in plane q, lo halves in
 // plane 8 + q), each a zero-haloed grid of (N+2) rows x ln_row(N) slots of 16 B (8 f16). A plane
 // is a multiple of 256 B (the LDS bank period), so the 16-B chunk of every plane of a slot sits in
@@ -77,7 +92,7 @@ __host__ __device__ constexpr int ln_lds_bytes(int N) { return 18 * ln_plane(N) 
 // or -1 for a spare column (N*N not a multiple of 16).
 template <int N>
 struct LnPixMap {
-  static constexpr int NN = N * N, NG = (NN + 15) / 16, RS = ln_row(N);
+  static constexpr int NN = N * N, NG = ln_groups(N), RS = ln_row(N);
   int slot[NG * 16];
   constexpr LnPixMap() : slot() {
     bool used[NN] = {};
@@ -127,11 +142,6 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
   asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
-  f32x2 r;
-  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 __device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {
   f32x2 r;
   asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -155,26 +165,40 @@ __device__ __forceinline__ float block_max(float m, float* red, int wave, int l)
   return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// One K chunk over the board's NG pixel groups: per group the B fragments (hi, lo) from the grid
-// (LDS; read two groups ahead; pb[g] = the lane's slot in bytes, coff = the chunk's plane and tap
-// offset) and acc[g] += ah*bh + al*bh + ah*bl. The MFMAs are inline asm with
-// the accumulator in place in AGPRs (srcC = vdst: back-to-back accumulation, no copies); INIT
-// starts the accumulators from 0. HALF: byte offset of the lo halves from the hi halves.
+// The lane's B fragments (hi, lo) of one group: grid + pb (the lane's slot in bytes) + coff (the
+// chunk's plane and tap offset); HALF = byte offset of the lo halves from the hi halves.
+template <int HALF>
+__device__ __forceinline__ void ln_load(h16x8 (&r)[2], const unsigned char* grid, int pb, int coff) {
+  const unsigned char* q = grid + pb + coff;
+  r[0] = *reinterpret_cast<const h16x8*>(q);
+  r[1] = *reinterpret_cast<const h16x8*>(q + HALF);
+}
+
+// Fill the ring with the first kLnPf groups of a chunk (at a layer start, after the barrier).
+template <int NG, int HALF>
+__device__ __forceinline__ void ln_prime(h16x8 (&rb)[kLnSlots][2], const unsigned char* grid, const int (&pb)[NG],
+                                         int coff) {
+#pragma unroll
+  for (int g = 0; g < kLnPf; ++g) ln_load<HALF>(rb[g], grid, pb[g], coff);
+}
+
+// One K chunk over the board's NG pixel groups: acc[g] += ah*bh + al*bh + ah*bl with the group's
+// B fragments from the ring, whose reads run kLnPf groups ahead and on into the next chunk
+// (coff_next; on the last chunk of a layer any in-grid offset: those reads are never consumed).
+// The MFMAs are inline asm with the accumulator in place in AGPRs (srcC = vdst: back-to-back
+// accumulation, no copies); INIT starts the accumulators from 0.
 template <int NG, bool INIT, int HALF>
 __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, const unsigned char* grid,
-                                         const int (&pb)[NG], int coff) {
-  h16x8 rb[3][2];
-  auto load = [&](int g, int slot) {
-    const unsigned char* q = grid + pb[g] + coff;
-    rb[slot][0] = *reinterpret_cast<const h16x8*>(q);
-    rb[slot][1] = *reinterpret_cast<const h16x8*>(q + HALF);
-  };
-  load(0, 0);
-  if (NG > 1) load(1, 1);
+                                         const int (&pb)[NG], int coff, int coff_next, h16x8 (&rb)[kLnSlots][2]) {
+  static_assert(NG % kLnSlots == 0, "ln_chunk: the ring slot of a group must not depend on the chunk");
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    if (g + 2 < NG) load(g + 2, (g + 2) % 3);
-    const h16x8 bh = rb[g % 3][0], bl = rb[g % 3][1];
+    const int gp = g + kLnPf;
+    if (gp < NG)
+      ln_load<HALF>(rb[gp % kLnSlots], grid, pb[gp], coff);
+    else
+      ln_load<HALF>(rb[gp % kLnSlots], grid, pb[gp - NG], coff_next);
+    const h16x8 bh = rb[g % kLnSlots][0], bl = rb[g % kLnSlots][1];
     if (INIT)
       asm volatile(
           "v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\t"
@@ -213,7 +237,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
                                                               const float* __restrict__ bt,
                                                               const float* __restrict__ bounds, int nlayers,
                                                               LnHeads hd, float* __restrict__ xout) {
-  constexpr int NN = N * N, RS = ln_row(N), NG = (NN + 15) / 16, PIX_IT = (NN + kLnThreads - 1) / kLnThreads;
+  constexpr int NN = N * N, RS = ln_row(N), NG = ln_groups(N), PIX_IT = (NN + kLnThreads - 1) / kLnThreads;
   constexpr int PL = ln_plane(N);
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned char* act = lds;                  // 16 planes [hi q | lo q][(N+2) x RS slots][16 B]
@@ -239,6 +263,28 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     valid |= (sl >= 0 ? 1u : 0u) << g;
   }
   auto is_valid = [&](int g) { return NN % 16 == 0 || ((valid >> g) & 1u); };
+
+  // the weights stream through a ring of kLnWpf + 1 chunks, kLnWpf chunks ahead of the MFMAs and
+  // on into the next layer (18 chunks per layer: the ring slot of chunk c is c % (kLnWpf + 1) in
+  // every layer), so no layer starts on an exposed L2 load
+  static_assert(18 % (kLnWpf + 1) == 0, "BK_LN_WPF: the ring must divide the 18 chunks of a layer");
+  h16x8 wq[kLnWpf + 1][2];  // issued here: in flight under the stem
+  {
+    const h16x8* w0 = wt + (wave * 2) * 64 + l;
+#pragma unroll
+    for (int c = 0; c < kLnWpf; ++c) {
+      wq[c][0] = w0[c * 8 * 64];
+      wq[c][1] = w0[c * 8 * 64 + 64];
+    }
+  }
+  // the stem's weights (3 chunks), scale and bias, in flight under the observation loads
+  h16x8 wsa[3][2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    wsa[j][0] = wstem[((j * 4 + wave) * 2) * 64 + l];
+    wsa[j][1] = wstem[((j * 4 + wave) * 2 + 1) * 64 + l];
+  }
+  const f32x4 s_stem = *reinterpret_cast<const f32x4*>(sstem + oc), b_stem = *reinterpret_cast<const f32x4*>(bstem + oc);
 
   // ---- stem input: the planar observation [8][N][N] of the board, scaled by its maximum, split
   const float* ob = obs + b * kStemCinX3 * NN;
@@ -273,15 +319,20 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 
   // ---- stem conv: 3 chunks; lane k-group ks of chunk j is tap 4j + ks (taps > 8 carry zero weights)
   f32x4 acc[NG];
+  h16x8 rb[kLnSlots][2];
+  {
+    auto toff = [&](int j) {
+      const int t = 4 * j + ks < 9 ? 4 * j + ks : 8;
+      return ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
+    };
+    ln_prime<NG, PL>(rb, sin, pb, toff(0));
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int t = 4 * j + ks < 9 ? 4 * j + ks : 8;
-    const int toff = ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
-    const h16x8 ah = wstem[((j * 4 + wave) * 2) * 64 + l], al = wstem[((j * 4 + wave) * 2 + 1) * 64 + l];
-    if (j == 0)
-      ln_chunk<NG, true, PL>(acc, ah, al, sin, pb, toff);
-    else
-      ln_chunk<NG, false, PL>(acc, ah, al, sin, pb, toff);
+    for (int j = 0; j < 3; ++j) {
+      if (j == 0)
+        ln_chunk<NG, true, PL>(acc, wsa[0][0], wsa[0][1], sin, pb, toff(0), toff(1), rb);
+      else
+        ln_chunk<NG, false, PL>(acc, wsa[j][0], wsa[j][1], sin, pb, toff(j), toff(j < 2 ? j + 1 : j), rb);
+    }
   }
   ln_mfma_drain();
   LNSTAMP(2, __builtin_amdgcn_s_memtime());
@@ -291,24 +342,19 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // reduction is needed before the split), split, and the packed halves kept in acc's registers
   // until every wave has finished reading the grid (bar 1), then written; the lane's max |y|
   // (unscaled) is returned for the next layer's bound. !OUT (the last conv): y stays in acc.
-  auto epilogue = [&](const float* sv, const float* bv, bool relu, bool residual, const f32x4 (&x0)[NG],
-                      bool out, int ex_out) {
-    f32x2 s01, s23, b01, b23;
-    s01.x = ldexpf(sv[oc], -ex);
-    s01.y = ldexpf(sv[oc + 1], -ex);
-    s23.x = ldexpf(sv[oc + 2], -ex);
-    s23.y = ldexpf(sv[oc + 3], -ex);
-    b01 = f32x2{bv[oc], bv[oc + 1]};
-    b23 = f32x2{bv[oc + 2], bv[oc + 3]};
-    const float up = ldexpf(1.0f, ex_out);
-    const f32x2 up2{up, up};
+  auto epilogue = [&](f32x4 sv, f32x4 bv, bool relu, bool residual, const f32x4 (&x0)[NG], bool out, int ex_out) {
+    // OUT folds the output scale 2^ex_out into s and bias (exact: powers of two), so y comes out
+    // scaled and goes straight to the split; the lane maximum is unscaled once at the end
+    const int k = out ? ex_out : 0;
+    const f32x2 s01{ldexpf(sv.x, k - ex), ldexpf(sv.y, k - ex)}, s23{ldexpf(sv.z, k - ex), ldexpf(sv.w, k - ex)};
+    const f32x2 b01{ldexpf(bv.x, k), ldexpf(bv.y, k)}, b23{ldexpf(bv.z, k), ldexpf(bv.w, k)};
     const float floor = relu ? 0.0f : -__builtin_inff();
     float mx = 0.0f;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       f32x2 y01 = pk_fma(f32x2{acc[g][0], acc[g][1]}, s01, b01);
       f32x2 y23 = pk_fma(f32x2{acc[g][2], acc[g][3]}, s23, b23);
-      if (residual) {
+      if (residual) {  // only without OUT (the last conv): x0 is unscaled
         y01 = pk_add(y01, f32x2{x0[g][0], x0[g][1]});
         y23 = pk_add(y23, f32x2{x0[g][2], x0[g][3]});
       }
@@ -316,17 +362,16 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       y23 = f32x2{fmaxf(y23.x, floor), fmaxf(y23.y, floor)};
       if (is_valid(g)) mx = fmaxf(fmaxf(mx, fmaxf(fabsf(y01.x), fabsf(y01.y))), fmaxf(fabsf(y23.x), fabsf(y23.y)));
       if (out) {
-        const f32x2 z01 = pk_mul(y01, up2), z23 = pk_mul(y23, up2);
         unsigned h0, h1, l0, l1;
-        split2(z01.x, z01.y, h0, l0);
-        split2(z23.x, z23.y, h1, l1);
+        split2(y01.x, y01.y, h0, l0);
+        split2(y23.x, y23.y, h1, l1);
         acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
                        __builtin_bit_cast(float, l1)};
       } else {
         acc[g] = f32x4{y01.x, y01.y, y23.x, y23.y};
       }
     }
-    return mx;
+    return ldexpf(mx, -k);
   };
   // the packed halves in acc -> the activation grid (channels oc..oc+3: plane oc/8 = 2 wave + ks/2,
   // bytes 8 (ks & 1) of the slot)
@@ -362,7 +407,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 #pragma unroll
     for (int g = 0; g < NG; ++g) x0[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the stem output itself is kept (unscaled) for the tower's final residual
-    const float mx = epilogue(sstem, bstem, true, false, x0, false, 0);
+    const float mx = epilogue(s_stem, b_stem, true, false, x0, false, 0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) x0[g] = acc[g];
     const float up = ldexpf(1.0f, ex_out);
@@ -388,33 +433,37 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   constexpr int kLayerBlocks = 18 * 4 * 2;  // (chunk, wave, part) blocks per layer
   for (int layer = 0; layer < nlayers; ++layer) {
     const h16x8* wl = wt + (size_t)layer * kLayerBlocks * 64 + (wave * 2) * 64 + l;
-    h16x8 ah = wl[0], al = wl[64];
+    const bool more = layer + 1 < nlayers;
+    // the layer's output scale and bias (folded BN) are loaded here, under the MFMA loop
+    const f32x4 sv = *reinterpret_cast<const f32x4*>(st + layer * 64 + oc);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + layer * 64 + oc);
     auto coff_of = [&](int c) {
       const int t = c >> 1;
       return (4 * (c & 1) + ks) * PL + ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
     };
-    {
-      const h16x8 nh = wl[8 * 64], nl = wl[8 * 64 + 64];
-      ln_chunk<NG, true, 8 * PL>(acc, ah, al, act, pb, coff_of(0));
-      ah = nh;
-      al = nl;
-    }
-    for (int c = 1; c < 18; ++c) {
-      h16x8 nh = ah, nl = al;
-      if (c + 1 < 18) {
-        nh = wl[(c + 1) * 8 * 64];
-        nl = wl[(c + 1) * 8 * 64 + 64];
+    ln_prime<NG, 8 * PL>(rb, act, pb, coff_of(0));
+#pragma unroll
+    for (int c = 0; c < 18; ++c) {
+      const int cn = c + kLnWpf, sn = cn % (kLnWpf + 1);
+      if (cn < 18) {
+        wq[sn][0] = wl[cn * 8 * 64];
+        wq[sn][1] = wl[cn * 8 * 64 + 64];
+      } else if (more) {  // the next layer's first chunks
+        wq[sn][0] = wl[kLayerBlocks * 64 + (cn - 18) * 8 * 64];
+        wq[sn][1] = wl[kLayerBlocks * 64 + (cn - 18) * 8 * 64 + 64];
       }
-      ln_chunk<NG, false, 8 * PL>(acc, ah, al, act, pb, coff_of(c));
-      ah = nh;
-      al = nl;
+      const h16x8* w = wq[c % (kLnWpf + 1)];
+      if (c == 0)
+        ln_chunk<NG, true, 8 * PL>(acc, w[0], w[1], act, pb, coff_of(0), coff_of(1), rb);
+      else
+        ln_chunk<NG, false, 8 * PL>(acc, w[0], w[1], act, pb, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
     }
     ln_mfma_drain();
     if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
     const bool last = layer + 1 == nlayers;
     if (!last) {
       const int ex_out = out_exp(layer + 1, max_in);
-      const float mx = epilogue(st + layer * 64, bt + layer * 64, !(layer & 1), false, x0, true, ex_out);
+      const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
       post_max(mx, (layer + 1) & 1);
       __syncthreads();  // every wave has finished reading the grid
       write_act();
@@ -422,7 +471,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       max_in = board_max((layer + 1) & 1);
       ex = ex_out;
     } else {
-      epilogue(st + layer * 64, bt + layer * 64, true, true, x0, false, 0);
+      epilogue(sv, bv, true, true, x0, false, 0);
     }
     if (layer < 8) LNSTAMP(5 + 2 * layer, __builtin_amdgcn_s_memtime());
   }
@@ -540,7 +589,9 @@ int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, co
   BK_REQUIRE(nlayers >= 1, "bk_leafnet_x3: at least one tower conv");
   BK_REQUIRE(bk_leafnet_x3_supported(N), "bk_leafnet_x3: N must be 14 or 20");
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
-  BK_REQUIRE(a16(wstem) && a16(wtower) && a16(wp) && a16(wv) && a16(out), "bk_leafnet_x3: 16-byte aligned buffers");
+  BK_REQUIRE(a16(wstem) && a16(wtower) && a16(sstem) && a16(bstem) && a16(stower) && a16(btower) && a16(wp) &&
+                 a16(wv) && a16(out),
+             "bk_leafnet_x3: 16-byte aligned buffers");
   if (B == 0) return BK_OK;
   {
     const void* fns[2] = {(const void*)k_leafnet_x3<14>, (const void*)k_leafnet_x3<20>};
