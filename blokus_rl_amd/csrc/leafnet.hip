@@ -74,8 +74,11 @@ constexpr int kLnPf = BK_LN_PF, kLnSlots = 5, kLnWpf = BK_LN_WPF;
 static_assert(kLnPf >= 1 && kLnPf < kLnSlots, "BK_LN_PF");
 __host__ __device__ constexpr int ln_groups(int N) { return ((N * N + 15) / 16 + kLnSlots - 1) / kLnSlots * kLnSlots; }
 
-// The layer input in LDS: 16 planes (hi halves of channels 8q..8q+7 in plane q, lo halves in
-// plane 8 + q), each a zero-haloed grid of (N+2) rows x ln_row(N) slots of 16 B (8 f16). A plane
+// The layer input in LDS: 16 planes, each a zero-haloed grid of (N+2) rows x ln_row(N) slots of
+// 16 B (8 f16). Channel octet o (channels 8o..8o+7) has its hi halves in plane 4 (o % 4) + 2 (o / 4)
+// and its lo halves in the next plane: the octets a lane's k-group ks reads (ks and 4 + ks) sit
+// in its own block of 4 planes, so one base register per group reaches every chunk's tap and
+// half with an immediate offset (< 3 planes + 2 rows). A plane
 // is a multiple of 256 B (the LDS bank period), so the 16-B chunk of every plane of a slot sits in
 // the same 4 banks, and the lanes of one ds_read_b128 lane group (16 distinct pixels of a group,
 // k-groups ks and ks^1) are conflict-free when their slots differ mod 16 (LnPixMap). The stem's
@@ -146,6 +149,18 @@ __device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {
   f32x2 r;
   asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
+}
+
+// max(m, |a|, |b|) in one VALU op (fmaxf would canonicalize every input first)
+__device__ __forceinline__ float max3_abs(float m, float a, float b) {
+  float r;
+  asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+// max(y, floor) as signed integers: y for floor = INT_MIN, relu(y) for floor = 0 (-0 -> +0),
+// one v_max_i32 (the float max would add a canonicalize per input)
+__device__ __forceinline__ float max_bits(float y, int floor) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(int, y), floor));
 }
 
 // the power of two that brings the largest magnitude m into [2^14, 2^15)
@@ -254,15 +269,20 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 
   // the lane's grid slot in each group, in bytes (a spare column reads slot 0 of the halo: zeros),
   // and the mask of groups where the lane's column is a board pixel
-  int pb[NG];
+  // ab[g] = the lane's B-read base: its slot + its k-group's plane block, less kBias so that
+  // every chunk's plane/tap offset is a non-negative immediate (no address VALU in the MFMA loop);
+  // a spare column reads at pixel (0, 0) (its MFMA column is never written out)
+  constexpr int kBias = (RS + 1) * 16;
+  int ab[NG];
   unsigned valid = 0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int sl = kLnPixMap<N>.slot[16 * g + n];
-    pb[g] = (sl >= 0 ? sl : 0) * 16;
+    ab[g] = (sl >= 0 ? sl : RS + 1) * 16 + ks * 4 * PL - kBias;
     valid |= (sl >= 0 ? 1u : 0u) << g;
   }
   auto is_valid = [&](int g) { return NN % 16 == 0 || ((valid >> g) & 1u); };
+  auto slot_b = [&](int g) { return ab[g] - ks * 4 * PL + kBias; };  // the lane's slot in group g, bytes
 
   // the weights stream through a ring of kLnWpf + 1 chunks, kLnWpf chunks ahead of the MFMAs and
   // on into the next layer (18 chunks per layer: the ring slot of chunk c is c % (kLnWpf + 1) in
@@ -323,15 +343,15 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   {
     auto toff = [&](int j) {
       const int t = 4 * j + ks < 9 ? 4 * j + ks : 8;
-      return ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
+      return ((t / 3 - 1) * RS + (t % 3 - 1)) * 16 + kBias - ks * 4 * PL;  // from ab: the stem grid has 2 planes
     };
-    ln_prime<NG, PL>(rb, sin, pb, toff(0));
+    ln_prime<NG, PL>(rb, sin, ab, toff(0));
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       if (j == 0)
-        ln_chunk<NG, true, PL>(acc, wsa[0][0], wsa[0][1], sin, pb, toff(0), toff(1), rb);
+        ln_chunk<NG, true, PL>(acc, wsa[0][0], wsa[0][1], sin, ab, toff(0), toff(1), rb);
       else
-        ln_chunk<NG, false, PL>(acc, wsa[j][0], wsa[j][1], sin, pb, toff(j), toff(j < 2 ? j + 1 : j), rb);
+        ln_chunk<NG, false, PL>(acc, wsa[j][0], wsa[j][1], sin, ab, toff(j), toff(j < 2 ? j + 1 : j), rb);
     }
   }
   ln_mfma_drain();
@@ -348,7 +368,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     const int k = out ? ex_out : 0;
     const f32x2 s01{ldexpf(sv.x, k - ex), ldexpf(sv.y, k - ex)}, s23{ldexpf(sv.z, k - ex), ldexpf(sv.w, k - ex)};
     const f32x2 b01{ldexpf(bv.x, k), ldexpf(bv.y, k)}, b23{ldexpf(bv.z, k), ldexpf(bv.w, k)};
-    const float floor = relu ? 0.0f : -__builtin_inff();
+    const int floor = relu ? 0 : (int)0x80000000u;
     float mx = 0.0f;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -358,9 +378,9 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         y01 = pk_add(y01, f32x2{x0[g][0], x0[g][1]});
         y23 = pk_add(y23, f32x2{x0[g][2], x0[g][3]});
       }
-      y01 = f32x2{fmaxf(y01.x, floor), fmaxf(y01.y, floor)};
-      y23 = f32x2{fmaxf(y23.x, floor), fmaxf(y23.y, floor)};
-      if (is_valid(g)) mx = fmaxf(fmaxf(mx, fmaxf(fabsf(y01.x), fabsf(y01.y))), fmaxf(fabsf(y23.x), fabsf(y23.y)));
+      y01 = f32x2{max_bits(y01.x, floor), max_bits(y01.y, floor)};
+      y23 = f32x2{max_bits(y23.x, floor), max_bits(y23.y, floor)};
+      if (is_valid(g)) mx = max3_abs(max3_abs(mx, y01.x, y01.y), y23.x, y23.y);
       if (out) {
         unsigned h0, h1, l0, l1;
         split2(y01.x, y01.y, h0, l0);
@@ -373,19 +393,21 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     }
     return ldexpf(mx, -k);
   };
-  // the packed halves in acc -> the activation grid (channels oc..oc+3: plane oc/8 = 2 wave + ks/2,
-  // bytes 8 (ks & 1) of the slot)
+  // the packed halves in acc -> the activation grid. The lane holds channels oc..oc+3 (hi, lo) of
+  // octet o = 2 wave + ks/2; the k-groups ks and ks^1 (rows of 16 lanes) hold the two halves of the
+  // octet's 16-B slot. v_permlane16_swap gives the even row both rows' hi halves and the odd row
+  // both lo halves, so each lane stores one 16-B slot (hi plane, or the lo plane next to it).
   auto write_act = [&]() {
+    const int o = 2 * wave + (ks >> 1);
+    unsigned char* base = act + ((o & 3) * 4 + (o >> 2) * 2 + (ks & 1)) * PL;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      if (is_valid(g)) {
-        unsigned char* dst = act + (2 * wave + (ks >> 1)) * PL + pb[g] + 8 * (ks & 1);
-        // bit_cast the whole vector: hipcc's __builtin_bit_cast of an ext_vector element reads
-        // element 0 whatever the index (ROCm 7.2)
-        const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);
-        *reinterpret_cast<u32x2*>(dst) = u32x2{w.x, w.y};
-        *reinterpret_cast<u32x2*>(dst + 8 * PL) = u32x2{w.z, w.w};
-      }
+      // bit_cast the whole vector: hipcc's __builtin_bit_cast of an ext_vector element reads
+      // element 0 whatever the index (ROCm 7.2)
+      const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);  // {hi 01, hi 23, lo 01, lo 23}
+      const auto r0 = __builtin_amdgcn_permlane16_swap(w.x, w.z, false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(w.y, w.w, false, false);
+      if (is_valid(g)) *reinterpret_cast<u32x4*>(base + slot_b(g)) = u32x4{r0[0], r1[0], r0[1], r1[1]};
     }
   };
   // the scale of a conv's output from the bound |y| <= A max_in + B (A = the largest row L1 norm
@@ -437,13 +459,18 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     // the layer's output scale and bias (folded BN) are loaded here, under the MFMA loop
     const f32x4 sv = *reinterpret_cast<const f32x4*>(st + layer * 64 + oc);
     const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + layer * 64 + oc);
+    // chunk c = (tap c/2, channel half c%2): the lane's octet 4 (c%2) + ks has its hi plane at
+    // ks*4 + 2 (c%2) (lo next to it), so from ab the offset is a compile-time immediate < 2^16
     auto coff_of = [&](int c) {
       const int t = c >> 1;
-      return (4 * (c & 1) + ks) * PL + ((t / 3 - 1) * RS + (t % 3 - 1)) * 16;
+      return 2 * (c & 1) * PL + ((t / 3 - 1) * RS + (t % 3 - 1)) * 16 + kBias;
     };
-    ln_prime<NG, 8 * PL>(rb, act, pb, coff_of(0));
+    ln_prime<NG, PL>(rb, act, ab, coff_of(0));
+    if (layer == 1) LNSTAMP(26, __builtin_amdgcn_s_memtime());
 #pragma unroll
     for (int c = 0; c < 18; ++c) {
+      if (layer == 1 && c == 1) LNSTAMP(27, __builtin_amdgcn_s_memtime());
+      if (layer == 1 && c == 9) LNSTAMP(28, __builtin_amdgcn_s_memtime());
       const int cn = c + kLnWpf, sn = cn % (kLnWpf + 1);
       if (cn < 18) {
         wq[sn][0] = wl[cn * 8 * 64];
@@ -454,9 +481,9 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       }
       const h16x8* w = wq[c % (kLnWpf + 1)];
       if (c == 0)
-        ln_chunk<NG, true, 8 * PL>(acc, w[0], w[1], act, pb, coff_of(0), coff_of(1), rb);
+        ln_chunk<NG, true, PL>(acc, w[0], w[1], act, ab, coff_of(0), coff_of(1), rb);
       else
-        ln_chunk<NG, false, 8 * PL>(acc, w[0], w[1], act, pb, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+        ln_chunk<NG, false, PL>(acc, w[0], w[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
     }
     ln_mfma_drain();
     if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
@@ -464,10 +491,15 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     if (!last) {
       const int ex_out = out_exp(layer + 1, max_in);
       const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
+      if (layer == 1) LNSTAMP(21, __builtin_amdgcn_s_memtime());
       post_max(mx, (layer + 1) & 1);
+      if (layer == 1) LNSTAMP(22, __builtin_amdgcn_s_memtime());
       __syncthreads();  // every wave has finished reading the grid
+      if (layer == 1) LNSTAMP(23, __builtin_amdgcn_s_memtime());
       write_act();
+      if (layer == 1) LNSTAMP(24, __builtin_amdgcn_s_memtime());
       __syncthreads();
+      if (layer == 1) LNSTAMP(25, __builtin_amdgcn_s_memtime());
       max_in = board_max((layer + 1) & 1);
       ex = ex_out;
     } else {
@@ -481,7 +513,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 #pragma unroll
     for (int g = 0; g < NG; ++g)
       if (is_valid(g))
-        *reinterpret_cast<f32x4*>(xout + (b * NN + ln_pixel<N>(pb[g] / 16)) * 64 + oc) = acc[g];
+        *reinterpret_cast<f32x4*>(xout + (b * NN + ln_pixel<N>(slot_b(g) / 16)) * 64 + oc) = acc[g];
   }
   __syncthreads();  // every wave is done with the activation grid: the heads' scratch reuses it
   float* hp = reinterpret_cast<float*>(act);  // [NN][4 waves][3]
@@ -502,7 +534,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         d[k] = a;
       }
       if (ks == 0 && is_valid(g)) {
-        float* dst = hp + (ln_pixel<N>(pb[g] / 16) * 4 + wave) * 3;
+        float* dst = hp + (ln_pixel<N>(slot_b(g) / 16) * 4 + wave) * 3;
         dst[0] = d[0];
         dst[1] = d[1];
         dst[2] = d[2];

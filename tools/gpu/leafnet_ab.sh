@@ -12,6 +12,6 @@ timeout -k 10 120 python tools/leafnet_ab.py dump $out/new.pt >> $out/dump.log 2
 python tools/leafnet_ab.py cmp $out/base.pt $out/new.pt
 BK_LIB=blokus_rl_amd/_lib/exp/libbase.so timeout -k 10 120 python tools/leafnet_bench.py 200 256 2> $out/time.err || exit 1
 timeout -k 10 120 python tools/leafnet_bench.py 200 256 2>> $out/time.err || exit 1
-if [ -f blokus_rl_amd/_lib/exp/liblnst.so ]; then
-  BK_LIB=blokus_rl_amd/_lib/exp/liblnst.so timeout -k 10 120 python tools/leafnet_bench.py 50 256 --stamps 2>> $out/time.err || exit 1
+if [ -f blokus_rl_amd/_lib/exp/libln_st.so ]; then
+  BK_LIB=blokus_rl_amd/_lib/exp/libln_st.so timeout -k 10 120 python tools/leafnet_bench.py 50 256 --stamps 2>> $out/time.err || exit 1
 fi

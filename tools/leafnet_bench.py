@@ -62,6 +62,18 @@ if "--stamps" in sys.argv:
         phases[names[i]] = float(np.median(d))
         prev = i
     res["phase_cycles_median"] = phases
+    epi = {}  # layer 1's epilogue: compute, wave max, barrier 1, grid writes, barrier 2
+    for i, nm in zip(range(21, 26), ("compute", "wave_max", "barrier1", "write_act", "barrier2")):
+        prev_i = 4 + 2 * 1 if i == 21 else i - 1
+        epi[nm] = float(np.median(rel[:, :, i] - rel[:, :, prev_i]))
+    res["layer1_epilogue_cycles_median"] = epi
+    # layer 1's MFMA loop: prime (from layer 0's epilogue end), chunk 0, chunks 1-8, chunks 9-17 + drain
+    res["layer1_loop_cycles_median"] = {
+        "prime": float(np.median(rel[:, :, 26] - rel[:, :, 5])),
+        "chunk0": float(np.median(rel[:, :, 27] - rel[:, :, 26])),
+        "chunks1_8": float(np.median(rel[:, :, 28] - rel[:, :, 27])),
+        "chunks9_17": float(np.median(rel[:, :, 6] - rel[:, :, 28])),
+    }
     res["total_cycles_median"] = float(np.median(rel[:, :, 29]))
     res["clock_ghz_median"] = float(np.median(clk))
     res["mfma_cycles_per_layer_floor"] = 18 * ng * 3 * 16
