@@ -232,8 +232,15 @@ __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, c
 }
 
 // the accumulators are written by MFMAs the compiler cannot see: wait out the MFMA write ->
-// VALU read latency before the epilogue reads them
-__device__ __forceinline__ void ln_mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+// VALU read latency before the epilogue reads them. Each accumulator then passes through an empty
+// asm that follows the wait (volatile asm keeps its order), so no read of it can be scheduled
+// above the wait (an 8-wave variant of this kernel read one too early without this).
+template <int NG>
+__device__ __forceinline__ void ln_mfma_drain(f32x4 (&acc)[NG]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < NG; ++g) asm volatile("" : "+a"(acc[g]));
+}
 
 struct LnHeads {
   const float *wp, *bp, *wv, *bv, *w1t, *b1, *w2, *b2;
@@ -258,7 +265,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   unsigned char* act = lds;                  // 16 planes [hi q | lo q][(N+2) x RS slots][16 B]
   unsigned char* sin = lds + 16 * PL;        // 2 planes: the stem input hi, lo
   float* red = reinterpret_cast<float*>(lds + 18 * PL);
-  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, n = l & 15, ks = l >> 4;
+  const int tid = threadIdx.x, l = tid & 63, n = l & 15, ks = l >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   const int oc = 16 * wave + 4 * ks;  // the lane's 4 output channels oc..oc+3 in the D fragments
   const size_t b = blockIdx.x;
   LNSTAMP(0, __builtin_amdgcn_s_memtime());
@@ -354,7 +362,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         ln_chunk<NG, false, PL>(acc, wsa[j][0], wsa[j][1], sin, ab, toff(j), toff(j < 2 ? j + 1 : j), rb);
     }
   }
-  ln_mfma_drain();
+  ln_mfma_drain(acc);
   LNSTAMP(2, __builtin_amdgcn_s_memtime());
 
   // Epilogue of a conv: y = acc * s + bias (+ x0) (ReLU), s = the inverse weight scale x 2^-ex_in.
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       else
         ln_chunk<NG, false, PL>(acc, w[0], w[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
     }
-    ln_mfma_drain();
+    ln_mfma_drain(acc);
     if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
     const bool last = layer + 1 == nlayers;
     if (!last) {
