@@ -235,12 +235,12 @@ __device__ __forceinline__ bool has_any_legal(const DevPreset& dp, const uint32_
   return false;
 }
 
-// Functional next state, in place on the LDS copy s (mirrors colosseumrl next_state as called
-// at blokus_wrapper.py:103-105): place action a for the player to move, retire the piece,
-// update the board hash, then hand the turn to the next colour in cyclic order that has a
-// legal move (a colour found without one is cached as dead); nobody -> game over.
-// Returns 0 on success, 1 if a is not legal (s untouched).
-__device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, int a, uint64_t* fa) {
+// Placement of action a by the player to move, in place on the LDS copy s: the cells, the
+// incremental board hash, the piece retired, the ply count. VALIDATE: check legality first
+// (returns 1, s untouched, if a is not legal); without it the caller vouches for a (the search's
+// stored children are legal by construction). Returns 0 on success.
+template <bool VALIDATE = true>
+__device__ __forceinline__ int place_action(const DevPreset& dp, uint32_t* s, int a, uint64_t* fa) {
   const int l = lane_id();
   const int p = (int)s[kWToMove];
   if (a < 0 || a >= dp.A) return 1;
@@ -248,10 +248,12 @@ __device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, in
   const uint64_t it = dp.items[ad & 0xFFFFu];
   const int c = (int)((ad >> 16) & 0xFFu);
   const int pc = (int)(ad >> 24);
-  const bool piece_ok = (s[kWPieces + p] >> pc) & 1u;
-  compute_fa(dp, s, p, fa);
-  const uint32_t v = eval_item(it, fa);
-  if (!piece_ok || !((v >> c) & 1u)) return 1;  // wave-uniform
+  if (VALIDATE) {
+    const bool piece_ok = (s[kWPieces + p] >> pc) & 1u;
+    compute_fa(dp, s, p, fa);
+    const uint32_t v = eval_item(it, fa);
+    if (!piece_ok || !((v >> c) & 1u)) return 1;  // wave-uniform
+  }
   const int r = (int)((it >> 16) & 31u);
   uint64_t hx = 0;
   if (l < 5) {
@@ -280,18 +282,38 @@ __device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, in
     s[kWPly] += 1u;
   }
   BK_BOARD_SYNC();
+  return 0;
+}
+
+// The turn after colour p's placement: the next colour in cyclic order that has a legal move (a
+// colour found without one is cached as dead); nobody -> game over. ANY(q): does colour q have a
+// legal placement on s.
+template <typename AnyLegal>
+__device__ __forceinline__ void advance_turn(const DevPreset& dp, uint32_t* s, int p, AnyLegal any) {
+  const int l = lane_id();
   uint32_t flags = s[kWFlags];
   int next = -1;
   for (int d = 1; d <= dp.P; ++d) {
     const int q = (p + d) % dp.P;
     if ((flags >> (kFlagDeadShift + q)) & 1u) continue;
-    if (has_any_legal(dp, s, q, fa)) { next = q; break; }
+    if (any(q)) { next = q; break; }
     flags |= 1u << (kFlagDeadShift + q);
   }
   if (next < 0) { flags |= kFlagOver; next = (p + 1) % dp.P; }
   BK_BOARD_SYNC();
   if (l == 0) { s[kWFlags] = flags; s[kWToMove] = (uint32_t)next; }
   BK_BOARD_SYNC();
+}
+
+// Functional next state, in place on the LDS copy s (mirrors colosseumrl next_state as called
+// at blokus_wrapper.py:103-105): place action a for the player to move, retire the piece,
+// update the board hash, then hand the turn to the next colour in cyclic order that has a
+// legal move (a colour found without one is cached as dead); nobody -> game over.
+// Returns 0 on success, 1 if a is not legal (s untouched).
+__device__ __forceinline__ int apply_action(const DevPreset& dp, uint32_t* s, int a, uint64_t* fa) {
+  const int p = (int)s[kWToMove];
+  if (place_action<true>(dp, s, a, fa)) return 1;
+  advance_turn(dp, s, p, [&](int q) { return has_any_legal(dp, s, q, fa); });
   return 0;
 }
 

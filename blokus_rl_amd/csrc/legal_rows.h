@@ -30,6 +30,9 @@ struct RowCtx {
 // forbidden and anchor accumulators), then legal = anchor & ~forbidden, validity masks, and the
 // W-bit field ORed into the board's LDS bitmask (two 32-bit ORs; the second is 0 unless the field
 // straddles a word).
+#ifdef BK_NOATOMIC  // timing experiment only (wrong masks): plain stores instead of LDS atomics
+#define atomicOr(p, v) (*(p) = (v))
+#endif
 template <int O, int WPB, int SPLIT>
 __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c, int wave, int& base) {
   constexpr OrientC oc = kOrient[O];
@@ -76,6 +79,88 @@ __device__ __forceinline__ void orient_all(const DevPreset& dp, const RowCtx& c,
                                            std::index_sequence<Os...>) {
   int base = 0;
   (orient_step<(int)Os, WPB, SPLIT>(dp, c, wave, base), ...);
+}
+
+// The row context of colour q on the board s (LDS) for lanes 0..N-1 (the board's rows); lanes
+// past N and rows past the board are masked by rowok. first: q has no cell yet.
+__device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32) {
+  const int l = lane_id();
+  const int N = dp.N;
+  const bool ok = l < N;
+  const int r = ok ? l : 0;
+  const uint32_t own = ok ? s[q * kMaxN + r] : 0u;
+  const uint32_t occ = ok ? (s[r] | s[kMaxN + r] | s[2 * kMaxN + r] | s[3 * kMaxN + r]) : 0u;
+  const uint32_t up = (ok && r > 0) ? s[q * kMaxN + r - 1] : 0u;
+  const uint32_t dn = (ok && r + 1 < N) ? s[q * kMaxN + r + 1] : 0u;
+  const bool first = __ballot(own != 0u) == 0ull;
+  uint32_t forb = 0u, anch = 0u;
+  if (ok) {
+    forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
+    if (first)
+      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+    else
+      anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
+  }
+  RowCtx c;
+  c.fr[0] = __brev(forb);
+  c.ar[0] = __brev(anch);
+#pragma unroll
+  for (int d = 1; d < 5; ++d) {
+    const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
+    c.fr[d] = __shfl(c.fr[0], src, kWave);
+    c.ar[d] = __shfl(c.ar[0], src, kWave);
+  }
+  c.r = r;
+  c.rN1 = r * (N + 1);
+  c.pieces = s[kWPieces + q];
+#pragma unroll
+  for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
+  c.mb = m32;
+  return c;
+}
+
+// Does the context's colour have a legal placement? The orientations of its unused pieces in
+// table order, each the same per-row test as orient_step, until the first one with a legal origin
+// (registers only: no table loads, no LDS).
+template <size_t... Os>
+__device__ __forceinline__ bool orient_any(const DevPreset& dp, const RowCtx& c, std::index_sequence<Os...>) {
+  bool found = false;
+  auto step = [&](auto oi) {
+    constexpr int O = decltype(oi)::value;
+    constexpr OrientC oc = kOrient[O];
+    if (found || oc.piece >= dp.num_pieces || !((c.pieces >> oc.piece) & 1u)) return;  // wave-uniform
+    uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
+    uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
+#pragma unroll
+    for (int k = 1; k < oc.n; ++k) {
+      bad |= c.fr[oc.dr[k]] << oc.dc[k];
+      good |= c.ar[oc.dr[k]] << oc.dc[k];
+    }
+    const uint32_t colmask = (1u << (dp.N - oc.w + 1)) - 1u;
+    const uint32_t v = __brev(good & ~bad) & colmask & c.rowok[oc.h];
+    found = __ballot(v != 0u) != 0ull;
+  };
+  (step(std::integral_constant<int, (int)Os>{}), ...);
+  return found;
+}
+__device__ __forceinline__ bool rows_any_legal(const DevPreset& dp, const uint32_t* s, int q) {
+  if (!s[kWPieces + q]) return false;
+  const RowCtx c = row_ctx(dp, s, q, nullptr);
+  if (__ballot((c.ar[0] & ~c.fr[0]) != 0u) == 0ull) return false;  // no free anchor cell
+  return orient_any(dp, c, std::make_index_sequence<kNumOrient>{});
+}
+
+// The legal-move bitmask of colour q built by all WPB waves of the workgroup (the state in LDS,
+// m32 zeroed here): wave w evaluates the orientations O with O % WPB == w, all OR into m32.
+template <int WPB>
+__device__ __forceinline__ void build_mask_rows_wg(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32,
+                                                   int wave) {
+  for (int i = threadIdx.x; i < dp.W32pad / 4; i += kWave * WPB)
+    reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const RowCtx c = row_ctx(dp, s, q, m32);
+  __syncthreads();
+  orient_all<WPB, 0>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+  __syncthreads();
 }
 
 // One board per wave (the state already in LDS): lanes 0..N-1 are the board's rows, the same

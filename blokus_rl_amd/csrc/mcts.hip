@@ -14,6 +14,9 @@
 // Each tree is touched by exactly one wave per kernel, so its table, node and child regions
 // need no atomics. All search arithmetic is float64 (the reference's pinned numpy 1.25 promotes
 // every float32 meeting a Python number to float64), compiled with -ffp-contract=off.
+// The per-tree stages run on one wave (the descent, the expansion) while the other waves of a
+// k_select workgroup wait at a workgroup barrier, so board-level handoffs are wave-scope.
+#define BK_BOARD_SYNC() ::bk::wave_lds_sync()
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -29,25 +32,37 @@ __global__ __launch_bounds__(64) void k_reset(DevMcts m, const int32_t* flags) {
   const int t = blockIdx.y;
   if (flags && !flags[t]) return;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m.TS) m.tab_key[(size_t)t * m.TS + i] = 0ull;
+  if (i < m.TS) m.tab[(size_t)t * m.TS + i] = TabEntry{0ull, 0u, 0};
   if (i == 0) { m.tree_nodes[t] = 0; m.tree_children[t] = 0; }
 }
 
-// grid T x 64 threads: one wave per tree
-__global__ __launch_bounds__(64) void k_select(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
-                                               const int32_t* __restrict__ active, double cpuct,
-                                               int32_t* __restrict__ status_out, float* __restrict__ obs,
-                                               uint64_t* __restrict__ mask_out) {
+// grid T x 256 threads: wave 0 descends, then the 4 waves build the leaf's legal bitmask (the
+// orientations split over the waves) and write its observation rows
+constexpr int kSelectWaves = 4;
+__global__ __launch_bounds__(64 * kSelectWaves) void k_select(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
+                                                              const int32_t* __restrict__ active, double cpuct,
+                                                              int32_t* __restrict__ status_out, float* __restrict__ obs,
+                                                              uint64_t* __restrict__ mask_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  select_tree(dp, m, blockIdx.x, roots, active, cpuct, status_out, obs, mask_out, lds);
+  __shared__ int status_sh;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave == 0) {
+    const int st = select_descend(dp, m, blockIdx.x, roots, active, cpuct, status_out, lds);
+    if (lane_id() == 0) status_sh = st;
+  }
+  __syncthreads();
+  select_leaf<kSelectWaves>(dp, m, blockIdx.x, status_sh, obs, mask_out, lds, wave);
 }
 
 // grid (T, kLeafBlocks) x 256 threads: workgroup c takes share c of the tree's legal ids
+#ifndef BK_LEAF_R
+#define BK_LEAF_R 1  // R x 4 ids per wave at a time (A/B knob)
+#endif
 __global__ __launch_bounds__(256) void k_leaf_logits(DevPreset dp, DevMcts m, const float* __restrict__ feat,
                                                      int64_t ldf, int F, const float* __restrict__ W,
                                                      const float* __restrict__ bias) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  leaf_logits_tree<1>(dp, m, blockIdx.x, blockIdx.y, kLeafBlocks, feat, ldf, F, W, bias, lds);
+  leaf_logits_tree<BK_LEAF_R>(dp, m, blockIdx.x, blockIdx.y, kLeafBlocks, feat, ldf, F, W, bias, lds);
 }
 
 // grid T x 64 threads
@@ -75,14 +90,12 @@ __global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restri
   }
   const uint32_t* s = roots + (size_t)t * kStateWords;
   const uint64_t key = table_key(s);
-  const int node = table_find(m, t, key, nullptr);
-  if (node < 0) {
+  int64_t off;
+  int K;
+  if (!table_find(m, t, key, off, K, nullptr)) {
     if (l == 0) { counts[t] = -1; atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrMissingRoot); }
     return;
   }
-  const size_t gn = (size_t)t * m.node_cap + node;
-  const int64_t off = m.node_child[gn];
-  const int K = m.node_K[gn];
   if (l == 0) counts[t] = K <= cap ? K : -K;
   const int Kc = K <= cap ? K : cap;
   if (mode == 1) {
@@ -149,6 +162,7 @@ int bk_debug_stamps(unsigned long long* out) {  // [2][4096][8] host copy
 
 int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_mcts** out) {
   BK_REQUIRE(ctx && out && trees > 0 && node_cap > 0 && child_cap >= trees, "bad argument");
+  BK_REQUIRE(child_cap / trees <= (int64_t)0xffffffff, "bk_mcts_create: child_cap / trees must fit 32 bits");
   BK_REQUIRE(ctx->d_items, "host-only context (created with device < 0)");
   *out = nullptr;
   bk_mcts* m = new bk_mcts();
@@ -163,19 +177,14 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
   const size_t T = (size_t)trees;
   const int W64 = ctx->dp.W64;
   int rc = hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-  if (!rc) rc = mcts_alloc(m, &d.tab_key, T * TS);
-  if (!rc) rc = mcts_alloc(m, &d.tab_node, T * TS);
+  if (!rc) rc = mcts_alloc(m, &d.tab, T * TS);
   if (!rc) rc = mcts_alloc(m, &d.tree_nodes, T);
   if (!rc) rc = mcts_alloc(m, &d.tree_children, T);
-  if (!rc) rc = mcts_alloc(m, &d.node_child, T * node_cap);
-  if (!rc) rc = mcts_alloc(m, &d.node_K, T * node_cap);
-  if (!rc) rc = mcts_alloc(m, &d.node_visits, T * node_cap);
   const size_t C = (size_t)d.child_cap_per_tree * T;
   if (!rc) rc = mcts_alloc(m, &d.ch_id, C);
   if (!rc) rc = mcts_alloc(m, &d.ch_N, C);
   if (!rc) rc = mcts_alloc(m, &d.ch_Q, C);
   if (!rc) rc = mcts_alloc(m, &d.ch_P, C);
-  if (!rc) rc = mcts_alloc(m, &d.path_node, T * kMaxDepth);
   if (!rc) rc = mcts_alloc(m, &d.path_child, T * kMaxDepth);
   if (!rc) rc = mcts_alloc(m, &d.path_pl, T * kMaxDepth);
   if (!rc) rc = mcts_alloc(m, &d.depth, T);
@@ -217,7 +226,7 @@ int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double 
   BK_REQUIRE(m && roots && leaf_status && obs, "bad argument");
   const DevPreset& dp = m->ctx->dp;
   const size_t lds = sizeof(uint32_t) * (size_t)(kStateWords + 2 * kMaxN + dp.W32pad);
-  hipLaunchKernelGGL(k_select, dim3(m->d.T), dim3(kWave), lds, (hipStream_t)stream, dp, m->d,
+  hipLaunchKernelGGL(k_select, dim3(m->d.T), dim3(kWave * kSelectWaves), lds, (hipStream_t)stream, dp, m->d,
                      (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask);
   return launch_check("k_select");
 }

@@ -16,7 +16,10 @@ constexpr int kMaxDepth = 96;
 constexpr int kExpandLdsIds = 2048;  // leaf ids staged in LDS up to this K
 constexpr int kGatherRegs = 16;      // logits gathered into registers: K <= 1024 in one round
 constexpr int kLeafCap = 2048;       // sparse leaf policy: legal ids per leaf (bk_mcts_leaf_logits)
-constexpr int kLeafBlocks = 4;       // workgroups per tree in k_leaf_logits
+#ifndef BK_LEAF_BLOCKS
+#define BK_LEAF_BLOCKS 4
+#endif
+constexpr int kLeafBlocks = BK_LEAF_BLOCKS;  // workgroups per tree in k_leaf_logits
 constexpr int kMaxFeat = 2048;       // policy-feature length staged in LDS
 constexpr int kLeafQ = 16;           // leaf logits: float4s of a W row a lane holds (F <= 1024)
 
@@ -30,21 +33,26 @@ static __device__ unsigned long long g_stamps[2][4096][8];
 #define BK_STAMP(k, i) do { } while (0)
 #endif  // > 84 = most placements a 4-player game can still make
 
+// One node of a tree's hash table, 16 B (one dwordx4 per lane per probe): the board key (0 =
+// empty slot), the node's first child in the tree's child region and its child count. A probe
+// thus yields the node's children directly; the visit sum the PUCT score needs (mcts.py:41-46
+// sums N over the children) comes from the children's N, loaded with the rest of their stats.
+struct __attribute__((aligned(16))) TabEntry {
+  unsigned long long key;
+  uint32_t off;  // first child, relative to the tree's child region
+  int32_t K;     // number of children
+};
+
 struct DevMcts {
   int T, node_cap, TS;  // TS = table slots per tree (power of two)
   int64_t child_cap_per_tree;
-  uint64_t* tab_key;    // [T*TS] 0 = empty
-  int32_t* tab_node;    // [T*TS] tree-local node index
-  int32_t* tree_nodes;  // [T]
+  TabEntry* tab;        // [T*TS]
+  int32_t* tree_nodes;  // [T] nodes in the tree (capacity check against node_cap)
   int64_t* tree_children;  // [T] children used in the tree's region
-  int64_t* node_child;  // [T*node_cap] offset into the child arrays (global index)
-  int32_t* node_K;      // [T*node_cap]
-  uint32_t* node_visits;  // [T*node_cap]  = sum of the children's N
   int32_t* ch_id;       // [T*cpt]
   uint32_t* ch_N;
   double* ch_Q;
   float* ch_P;
-  int32_t* path_node;   // [T*kMaxDepth] tree-local node
   int64_t* path_child;  // [T*kMaxDepth] global child index
   int32_t* path_pl;     // [T*kMaxDepth] player to move at the child (scores index)
   int32_t* depth;       // [T]
@@ -66,30 +74,34 @@ __device__ __forceinline__ uint64_t table_key(const uint32_t* s) {
   return h ? h : 1ull;
 }
 
-// Wave-parallel linear probe; returns the tree-local node or -1 (key absent).
-__device__ __forceinline__ int table_find(const DevMcts& m, int t, uint64_t key, int* free_slot) {
+// Wave-parallel linear probe, 64 whole entries per round trip. Found: true, the node's child
+// offset (global) and count. Absent: false and *free_slot = the first empty slot of the probe
+// sequence (-1 if the table is full).
+__device__ __forceinline__ bool table_find(const DevMcts& m, int t, uint64_t key, int64_t& off, int& K,
+                                           int* free_slot) {
   const int l = lane_id();
   const uint32_t mask = (uint32_t)m.TS - 1u;
   const uint32_t start = (uint32_t)(key ^ (key >> 29)) & mask;
-  const uint64_t* keys = m.tab_key + (size_t)t * m.TS;
+  const TabEntry* tab = m.tab + (size_t)t * m.TS;
   for (int p0 = 0; p0 < m.TS; p0 += kWave) {
     const uint32_t slot = (start + (uint32_t)(p0 + l)) & mask;
-    const uint64_t k = keys[slot];
-    const uint64_t hit = __ballot(k == key);
-    const uint64_t emp = __ballot(k == 0ull);
+    const TabEntry e = tab[slot];
+    const uint64_t hit = __ballot(e.key == key);
+    const uint64_t emp = __ballot(e.key == 0ull);
     if (hit) {
       const int src = __ffsll((unsigned long long)hit) - 1;
-      const int slot_hit = readlane_i((int)slot, src);
-      return m.tab_node[(size_t)t * m.TS + slot_hit];
+      off = (int64_t)t * m.child_cap_per_tree + (uint32_t)readlane_i((int)e.off, src);
+      K = readlane_i(e.K, src);
+      return true;
     }
     if (emp) {
       const int src = __ffsll((unsigned long long)emp) - 1;
       if (free_slot) *free_slot = readlane_i((int)slot, src);
-      return -1;
+      return false;
     }
   }
   if (free_slot) *free_slot = -1;
-  return -1;
+  return false;
 }
 
 // argmax over (value, index): larger value wins, ties -> smaller index (np.argmax's first max).
@@ -117,53 +129,80 @@ __device__ __forceinline__ void wave_argmax(double& best, int& bi) {
   best = __longlong_as_double((long long)u);
 }
 
-// PUCT choice at a node (mcts.py:41-46): argmax_i Q_i + cpuct*P_i*sqrt(sum N + 1e-6)/(1+N_i).
-__device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, uint32_t visits, double cp) {
+// PUCT choice at a node (mcts.py:41-46): argmax_i Q_i + cpuct*P_i*sqrt(sum N + 1e-6)/(1+N_i);
+// also returns the chosen child's action id. Up to kSelB * 64 children (every 20x20 node) in one
+// memory round trip: each lane loads all its children's (P, N, Q, id) first, the visit sum is
+// the wave's integer sum of N, then the lane scans its children in index order.
+constexpr int kSelB = 12;
+__device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, double cp, int& id_out) {
   const int l = lane_id();
-  const double sq = sqrt((double)visits + 1e-6);
   double best = -INFINITY;
-  int bi = 0x7fffffff;
+  int bi = 0x7fffffff, bid = 0;
   const float* P = m.ch_P + off;
   const uint32_t* Nn = m.ch_N + off;
   const double* Q = m.ch_Q + off;
-  int i = l;
-  for (; i + kWave < K; i += 2 * kWave) {  // two children per lane per trip: loads overlap
-    const float p0 = P[i], p1 = P[i + kWave];
-    const uint32_t n0 = Nn[i], n1 = Nn[i + kWave];
-    const double q0 = Q[i], q1 = Q[i + kWave];
-    const double h0 = q0 + ((cp * (double)p0) * sq) / (1.0 + (double)n0);
-    const double h1 = q1 + ((cp * (double)p1) * sq) / (1.0 + (double)n1);
-    if (h0 > best) { best = h0; bi = i; }
-    if (h1 > best) { best = h1; bi = i + kWave; }
-  }
-  if (i < K) {
-    const double h = Q[i] + ((cp * (double)P[i]) * sq) / (1.0 + (double)Nn[i]);
-    if (h > best) { best = h; bi = i; }
+  const int32_t* ID = m.ch_id + off;
+  if (K <= kSelB * kWave) {
+    float p[kSelB];
+    uint32_t nn[kSelB];
+    double q[kSelB];
+    int32_t id[kSelB];
+    // unconditional loads at a clamped index (K >= 1), so the compiler issues all of them before
+    // the first wait; lanes past K are masked out of the sum and the scan
+#pragma unroll
+    for (int u = 0; u < kSelB; ++u) {
+      const int i = min(l + u * kWave, K - 1);
+      p[u] = P[i];
+      nn[u] = Nn[i];
+      q[u] = Q[i];
+      id[u] = ID[i];
+    }
+    // every load issued before the first wait (one round trip): the compiler would otherwise
+    // wait for N's loads (the visit sum) before issuing the others
+#pragma unroll
+    for (int u = 0; u < kSelB; ++u) asm volatile("" : "+v"(p[u]), "+v"(nn[u]), "+v"(q[u]), "+v"(id[u]));
+    uint32_t vs = 0u;
+#pragma unroll
+    for (int u = 0; u < kSelB; ++u) vs += l + u * kWave < K ? nn[u] : 0u;
+    const double sq = sqrt((double)(uint32_t)wave_sum((int)vs) + 1e-6);
+#pragma unroll
+    for (int u = 0; u < kSelB; ++u) {
+      const int i = l + u * kWave;
+      if (i < K) {
+        const double h = q[u] + ((cp * (double)p[u]) * sq) / (1.0 + (double)nn[u]);
+        if (h > best) { best = h; bi = i; bid = id[u]; }
+      }
+    }
+  } else {  // two passes: the visit sum, then the scan
+    uint32_t vs = 0u;
+    for (int i = l; i < K; i += kWave) vs += Nn[i];
+    const double sq = sqrt((double)(uint32_t)wave_sum((int)vs) + 1e-6);
+    for (int i = l; i < K; i += kWave) {
+      const double h = Q[i] + ((cp * (double)P[i]) * sq) / (1.0 + (double)Nn[i]);
+      if (h > best) { best = h; bi = i; bid = ID[i]; }
+    }
   }
   wave_argmax(best, bi);
+  id_out = readlane_i(bid, bi & (kWave - 1));  // the owning lane's best is the wave's best
   return bi;
 }
 
-// k_select's work on tree t, by one wave (k_sims runs it too): lds = kStateWords + 2 kMaxN +
-// W32pad words. Returns the leaf status (wave-uniform): 0 inactive tree or error, 1 a leaf for the
-// net, 2 a terminal board. status_out, obs and mask_out may be null.
-__device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m, int t,
-                                           const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
-                                           double cpuct, int32_t* __restrict__ status_out, float* __restrict__ obs,
-                                           uint64_t* __restrict__ mask_out, uint32_t* lds) {
+// k_select's descent on tree t, by one wave: from the root to a board not in the tree or a
+// terminal board, the path recorded (mcts.py:37-50); the leaf state stays in LDS for select_leaf.
+// lds = kStateWords + 2 kMaxN + W32pad words. Returns the leaf status (wave-uniform): 0 inactive
+// tree or error, 1 a leaf for the net, 2 a terminal board.
+__device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts& m, int t,
+                                              const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
+                                              double cpuct, int32_t* __restrict__ status_out, uint32_t* lds) {
   uint32_t* s = lds;
   uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
-  uint32_t* m32 = lds + kStateWords + 2 * kMaxN;
   const int l = lane_id();
-  const int obs_len = 2 * dp.P * dp.N * dp.N;
   if (active && !active[t]) {
     if (l == 0) {
       m.leaf_status[t] = 0;
       if (status_out) status_out[t] = 0;
       m.depth[t] = 0;
     }
-    if (obs)
-      for (int i = l; i < obs_len; i += kWave) obs[(size_t)t * obs_len + i] = 0.0f;
     return 0;
   }
   BK_STAMP(0, 0);
@@ -173,20 +212,39 @@ __device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m
   double cp = cpuct;
   int depth = 0, err = 0;
   long long scanned = 0;
+#ifdef BK_STAMPS
+  unsigned long long t_probe = 0, t_child = 0, t_apply = 0;
+#define BK_TACC(v, stmt)                                         \
+  do {                                                           \
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime(); \
+    stmt;                                                        \
+    v += __builtin_amdgcn_s_memtime() - t0_;                     \
+  } while (0)
+#else
+#define BK_TACC(v, stmt) \
+  do {                   \
+    stmt;                \
+  } while (0)
+#endif
   for (;;) {
-    const int node = table_find(m, t, table_key(s), nullptr);
-    if (node < 0) break;
-    const size_t gn = (size_t)t * m.node_cap + node;
-    const int64_t off = m.node_child[gn];
-    const int Kn = m.node_K[gn];
+    int64_t off;
+    int Kn;
+    bool found;
+    BK_TACC(t_probe, found = table_find(m, t, table_key(s), off, Kn, nullptr));
+    if (!found) break;
+    if (Kn <= 0) { err |= kErrIllegal; break; }  // a stored node always has a legal move
     scanned += Kn;
-    const int ci = select_child(m, off, Kn, m.node_visits[gn], cp);
-    const int a = m.ch_id[off + ci];
+    int a, ci;
+    BK_TACC(t_child, ci = select_child(m, off, Kn, cp, a));
     if (depth >= kMaxDepth) { err |= kErrDepth; break; }
-    if (apply_action(dp, s, a, fa)) { err |= kErrIllegal; break; }
+    // the child's action is legal by construction (its id came from the node's legal mask)
+    const int p = (int)s[kWToMove];
+    int bad;
+    BK_TACC(t_apply, bad = place_action<false>(dp, s, a, fa);
+            if (!bad) advance_turn(dp, s, p, [&](int q) { return rows_any_legal(dp, s, q); }));
+    if (bad) { err |= kErrIllegal; break; }
     if (l == 0) {
       const size_t pi = (size_t)t * kMaxDepth + depth;
-      m.path_node[pi] = node;
       m.path_child[pi] = off + ci;
       m.path_pl[pi] = (int)s[kWToMove];
     }
@@ -194,8 +252,15 @@ __device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m
     cp = 1.0;  // the recursive call of mcts.py:50 passes no cpuct
   }
   BK_STAMP(0, 2);
+#ifdef BK_STAMPS
+  if (lane_id() == 0 && blockIdx.x < 4096) {
+    g_stamps[0][blockIdx.x][6] = t_probe;
+    g_stamps[0][blockIdx.x][7] = t_child;
+    g_stamps[1][blockIdx.x][7] = t_apply;  // (slot 7 of the expand record is free)
+  }
+#endif
+#undef BK_TACC
   int status;
-  float* o = obs ? obs + (size_t)t * obs_len : nullptr;
   if (err) {
     status = 0;
   } else if (s[kWFlags] & kFlagOver) {
@@ -203,23 +268,53 @@ __device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m
     if (l == 0) terminal_scores(dp, s, m.leaf_scores + (size_t)t * kMaxP);
   } else {
     status = 1;
-    build_mask_rows(dp, s, (int)s[kWToMove], m32);
+  }
+  if (l == 0) {
+    m.leaf_status[t] = status;
+    if (status_out) status_out[t] = status;
+    m.depth[t] = depth;
+    atomicAdd(&m.counters[kCtrLevels], (unsigned long long)depth);
+    atomicAdd(&m.counters[kCtrScanned], (unsigned long long)scanned);
+    if (status == 2) atomicAdd(&m.counters[kCtrTerminal], 1ull);
+    if (err) atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
+  }
+  return status;
+}
+
+// The leaf of a descent (state in LDS), by the NW waves of the workgroup (wave = this one's
+// index; 1 = the descending wave alone): for a leaf (status 1) the mover's legal bitmask (the
+// orientations split over the waves) and the leaf state to global memory, and for every tree
+// the observation rows the net reads (zeros unless status 1). obs and mask_out may be null.
+template <int NW>
+__device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& m, int t, int status,
+                                            float* __restrict__ obs, uint64_t* __restrict__ mask_out, uint32_t* lds,
+                                            int wave) {
+  const uint32_t* s = lds;
+  uint32_t* m32 = lds + kStateWords + 2 * kMaxN;
+  const int l = lane_id(), tid = wave * kWave + l;
+  const int obs_len = 2 * dp.P * dp.N * dp.N;
+  if (status == 1) {
+    if (NW == 1)
+      build_mask_rows(dp, s, (int)s[kWToMove], m32);
+    else
+      build_mask_rows_wg<NW>(dp, s, (int)s[kWToMove], m32, wave);
     BK_STAMP(0, 3);
     uint64_t* mo = m.leaf_mask + (size_t)t * dp.W64;
     uint64_t* mo2 = mask_out ? mask_out + (size_t)t * dp.W64 : nullptr;
-    for (int j = l; j < dp.W64; j += kWave) {
+    for (int j = tid; j < dp.W64; j += NW * kWave) {
       const uint64_t w = (uint64_t)m32[2 * j] | ((uint64_t)m32[2 * j + 1] << 32);
       mo[j] = w;
       if (mo2) mo2[j] = w;
     }
-    store_state(m.leaf_state + (size_t)t * kStateWords, s);
+    if (wave == 0) store_state(m.leaf_state + (size_t)t * kStateWords, s);
   }
   BK_STAMP(0, 4);
-  // observation row (zeros unless the leaf needs the net): lane = (plane, board row), the row's
+  // observation row (zeros unless the leaf needs the net): thread = (plane, board row), the row's
   // N floats as float4 stores when N is a multiple of 4 (no per-cell index arithmetic)
+  float* o = obs ? obs + (size_t)t * obs_len : nullptr;
   const int tm = (int)s[kWToMove];
   const int rows = 2 * dp.P * dp.N;
-  for (int pr = l; o && pr < rows; pr += kWave) {
+  for (int pr = tid; o && pr < rows; pr += NW * kWave) {
     const int plane = pr / dp.N, r = pr - plane * dp.N;
     uint32_t bits = 0u;
     if (status == 1) bits = plane < dp.P ? s[plane * kMaxN + r] : ((plane - dp.P) == tm ? dp.full_row : 0u);
@@ -233,15 +328,15 @@ __device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m
     }
   }
   BK_STAMP(0, 5);
-  if (l == 0) {
-    m.leaf_status[t] = status;
-    if (status_out) status_out[t] = status;
-    m.depth[t] = depth;
-    atomicAdd(&m.counters[kCtrLevels], (unsigned long long)depth);
-    atomicAdd(&m.counters[kCtrScanned], (unsigned long long)scanned);
-    if (status == 2) atomicAdd(&m.counters[kCtrTerminal], 1ull);
-    if (err) atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
-  }
+}
+
+// k_select's work on tree t by one wave (k_sims, k_sims_const): descent + leaf.
+__device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m, int t,
+                                           const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
+                                           double cpuct, int32_t* __restrict__ status_out, float* __restrict__ obs,
+                                           uint64_t* __restrict__ mask_out, uint32_t* lds) {
+  const int status = select_descend(dp, m, t, roots, active, cpuct, status_out, lds);
+  select_leaf<1>(dp, m, t, status, obs, mask_out, lds, 0);
   return status;
 }
 
@@ -387,19 +482,32 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
 // prior_mode 1: logp holds the prior itself at the legal ids (test hook: identical P fed to the
 //               reference and to this engine).
 // k_expand_backup's work on tree t, by one wave (k_sims runs it too): lds = W32pad + kExpandLdsIds words
+// The tree's scalars, the table probe, the logits and the path records are loaded in as few
+// dependent round trips as the data allows: (1) status, depth, node/child counters, leaf key and
+// K together; (2) the probe, the logit gather and the path records together; (3) the path
+// children's N and Q; then the stores.
 __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& m, int t, const float* __restrict__ logp,
                                             const float* __restrict__ values, int prior_mode, uint32_t* lds) {
   uint32_t* m32 = lds;  // W32pad words
   __shared__ double vsh[kMaxP];
   const int l = lane_id();
+  const bool sparse = prior_mode == 2;
+  // (1) independent per-tree loads
   const int status = m.leaf_status[t];
+  const int depth = m.depth[t];
+  const int node = m.tree_nodes[t];
+  const int64_t used = m.tree_children[t];
+  const int leafK = sparse ? m.leaf_K[t] : 0;
+  const uint64_t key = table_key(m.leaf_state + (size_t)t * kStateWords);
   if (status == 0) return;
   BK_STAMP(1, 0);
+  // (2a) the path records (lane d < depth: level d), issued before the expansion's loads
+  const size_t pi = (size_t)t * kMaxDepth + l;
+  const bool on_path = l < depth;  // depth <= kMaxDepth = 96: levels 64.. are handled below
+  const int64_t pchild = on_path ? m.path_child[pi] : 0;
+  const int ppl = on_path ? m.path_pl[pi] : 0;
   if (status == 1) {
-    const bool sparse = prior_mode == 2;
     int err = 0;
-    const int node = m.tree_nodes[t];
-    const int64_t used = m.tree_children[t];
     const int64_t room = m.child_cap_per_tree - used;
     const int64_t off = (int64_t)t * m.child_cap_per_tree + used;
     int32_t* ids_lds = reinterpret_cast<int32_t*>(m32 + dp.W32pad);
@@ -408,7 +516,7 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
     bool in_lds;
     BK_STAMP(1, 1);
     if (sparse) {
-      K = m.leaf_K[t];
+      K = leafK;
       in_lds = true;  // the ids are in leaf_ids: write them into the child region below
       if (K > kLeafCap) err |= kErrLeafCap;
     } else {
@@ -430,26 +538,30 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
     BK_STAMP(1, 2);
     if (node >= m.node_cap) err |= kErrTable;
     if (K > room) err |= kErrChildPool;
+    // (2b) the logit gather (all of a lane's loads issued before any is used, K <= 64 *
+    // kGatherRegs), beside the table probe below; dense modes gather logp[cid[i]], the sparse
+    // mode reads its logits in id order
+    const float* lp = sparse ? m.leaf_logit + (size_t)t * kLeafCap : logp + (size_t)t * dp.A;
+    const int32_t* cid = sparse ? m.leaf_ids + (size_t)t * kLeafCap : (in_lds ? ids_lds : m.ch_id + off);
+    auto logit = [&](int i) { return sparse ? lp[i] : lp[cid[i]]; };
+    float x[kGatherRegs];
+    int32_t xid[kGatherRegs];
+#pragma unroll
+    for (int j = 0; j < kGatherRegs; ++j) {
+      const int i = l + j * kWave;
+      const bool ok = !err && i < K;
+      x[j] = ok ? logit(i) : -INFINITY;
+      xid[j] = ok && in_lds ? cid[i] : 0;
+    }
     int free_slot = -1;
-    const uint64_t key = table_key(m.leaf_state + (size_t)t * kStateWords);
     if (!err) {
-      const int found = table_find(m, t, key, &free_slot);
-      if (found >= 0 || free_slot < 0) err |= kErrTable;
+      int64_t foff;
+      int fK;
+      if (table_find(m, t, key, foff, fK, &free_slot) || free_slot < 0) err |= kErrTable;
     }
     BK_STAMP(1, 3);
     if (!err) {
-      // dense modes gather logp[cid[i]]; the sparse mode reads its logits in id order
-      const float* lp = sparse ? m.leaf_logit + (size_t)t * kLeafCap : logp + (size_t)t * dp.A;
-      const int32_t* cid = sparse ? m.leaf_ids + (size_t)t * kLeafCap : (in_lds ? ids_lds : m.ch_id + off);
-      auto logit = [&](int i) { return sparse ? lp[i] : lp[cid[i]]; };
-      // all of a lane's gathers issued before any is used (K <= 64 * kGatherRegs)
-      float x[kGatherRegs];
       float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < kGatherRegs; ++j) {
-        const int i = l + j * kWave;
-        x[j] = i < K ? logit(i) : -INFINITY;
-      }
 #pragma unroll
       for (int j = 0; j < kGatherRegs; ++j) mx = fmaxf(mx, x[j]);
       for (int i = l + kGatherRegs * kWave; i < K; i += kWave) mx = fmaxf(mx, logit(i));
@@ -470,7 +582,7 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
       for (int j = 0; j < kGatherRegs; ++j) {
         const int i = l + j * kWave;
         if (i < K) {
-          if (in_lds) m.ch_id[off + i] = cid[i];
+          if (in_lds) m.ch_id[off + i] = xid[j];
           m.ch_N[off + i] = 0u;
           m.ch_Q[off + i] = 0.0;
           m.ch_P[off + i] = x[j];
@@ -484,12 +596,11 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
         m.ch_P[off + i] = prior_mode != 1 ? expf((xi - mx) - lse) : xi;
       }
       if (l == 0) {
-        const size_t gn = (size_t)t * m.node_cap + node;
-        m.node_child[gn] = off;
-        m.node_K[gn] = K;
-        m.node_visits[gn] = 0u;
-        m.tab_key[(size_t)t * m.TS + free_slot] = key;
-        m.tab_node[(size_t)t * m.TS + free_slot] = node;
+        TabEntry e;
+        e.key = key;
+        e.off = (uint32_t)used;
+        e.K = K;
+        m.tab[(size_t)t * m.TS + free_slot] = e;
         m.tree_nodes[t] = node + 1;
         m.tree_children[t] = used + K;
         atomicAdd(&m.counters[kCtrExpanded], 1ull);
@@ -504,16 +615,22 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
   }
   BK_STAMP(1, 4);
   BK_BOARD_SYNC();
-  const int depth = m.depth[t];
-  for (int d = l; d < depth; d += kWave) {
-    const size_t pi = (size_t)t * kMaxDepth + d;
-    const int64_t ci = m.path_child[pi];
-    const double v = vsh[m.path_pl[pi]];
+  // (3) the backup (mcts.py:53-56): each path child of the descent, one lane per level
+  if (on_path) {
+    const double v = vsh[ppl];
+    const uint32_t n = m.ch_N[pchild];
+    const double q = m.ch_Q[pchild];
+    m.ch_Q[pchild] = ((double)n * q + v) / (double)(n + 1u);
+    m.ch_N[pchild] = n + 1u;
+  }
+  for (int d = l + kWave; d < depth; d += kWave) {  // levels 64..kMaxDepth-1 (never at 20x20)
+    const size_t pd = (size_t)t * kMaxDepth + d;
+    const int64_t ci = m.path_child[pd];
+    const double v = vsh[m.path_pl[pd]];
     const uint32_t n = m.ch_N[ci];
     const double q = m.ch_Q[ci];
     m.ch_Q[ci] = ((double)n * q + v) / (double)(n + 1u);
     m.ch_N[ci] = n + 1u;
-    m.node_visits[(size_t)t * m.node_cap + m.path_node[pi]] += 1u;
   }
   BK_STAMP(1, 5);
 }

@@ -1,16 +1,20 @@
 """Diagnostic: per-phase cycle shares of k_select / k_expand_backup from the BK_STAMPS build
-(BK_LIB=blokus_rl_amd/_lib/diag/libblokus_hip_diag.so). Runs uninformed self-play plies."""
+(BK_LIB=blokus_rl_amd/_lib/diag/libblokus_hip_diag.so). Runs self-play plies with the bench's
+ResNet leaf net (or, with --dumbnet, the uninformed search), then stamps 30 simulations."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from blokus_rl_amd import engine
 from blokus_rl_amd.engine import Engine
-from blokus_rl_amd.nets import DumbNet
+from blokus_rl_amd.nets import DumbNet, build_model
 from blokus_rl_amd.alphazero.selfplay import SelfPlay
 
 eng = Engine(20, 4, 5)
-sp = SelfPlay(eng, DumbNet(20, 4, eng.A), 256, num_sims=100, seed=0, continuous=True)
-sp.play_ply(); sp.play_ply()
+torch.manual_seed(0)
+net = DumbNet(20, 4, eng.A) if "--dumbnet" in sys.argv else build_model("resnet", 20, 4, eng.A, num_res_blocks=5)
+sp = SelfPlay(eng, net.to(eng.device).eval(), 256, num_sims=100, seed=1234, continuous=True)
+for _ in range(4):
+    sp.play_ply()
 lib = engine.load_library()
 lib.bk_debug_stamps.argtypes = [ctypes.c_void_p]
 acc = {0: [], 1: []}
@@ -30,3 +34,6 @@ for k, names in ((0, ["load", "descent", "build_mask", "mask+state store", "obs 
           "(s_memtime ticks)")
     for i, n in enumerate(names):
         print(f"   {n:18s} median {int(np.median(d[:, :, i])):8d}  mean {d[:, :, i].mean():10.0f}")
+    if k == 0:  # the descent's parts, summed over its levels
+        for n, v in (("  probe", a[:, :, 6]), ("  select_child", a[:, :, 7]), ("  apply_action", np.stack(acc[1])[:, :, 7])):
+            print(f"   {n:18s} median {int(np.median(v)):8d}  mean {v.mean():10.0f}")
