@@ -285,13 +285,26 @@ class SelfPlay:
             self.mcts.expand_backup(out, v, prior_mode=0)
 
     def _sim_graph(self):
+        """SIM_GRAPH_SIMS simulations captured once. With the sparse policy head the search half of
+        a simulation and the next one's descent are one launch (bk_mcts_leaf_step): select, then
+        SIM_GRAPH_SIMS x {net, leaf_step (+ select, except the last)} — the trees of the per-stage
+        launches, bitwise (tests/test_sims_gpu.py)."""
         if self._graph is None:
             self._g_roots = self.roots.clone()
             self._g_active = self.active.clone()
+            ev = self.evaluator
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for _ in range(self.SIM_GRAPH_SIMS):
-                    self._sim_body()
+                if ev.model is not None and ev.sparse:
+                    _, obs, _ = self.mcts.select(self._g_roots, self._g_active, self.cpuct)
+                    for i in range(self.SIM_GRAPH_SIMS):
+                        out, v = ev._forward(obs)
+                        last = i == self.SIM_GRAPH_SIMS - 1
+                        self.mcts.leaf_step(out, ev.policy_w, ev.policy_b, v, None if last else self._g_roots,
+                                            self._g_active, self.cpuct)
+                else:
+                    for _ in range(self.SIM_GRAPH_SIMS):
+                        self._sim_body()
             self._graph = g
         return self._graph
 

@@ -17,6 +17,7 @@
 // The per-tree stages run on one wave (the descent, the expansion) while the other waves of a
 // k_select workgroup wait at a workgroup barrier, so board-level handoffs are wave-scope.
 #define BK_BOARD_SYNC() ::bk::wave_lds_sync()
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -70,6 +71,49 @@ __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, c
                                                       const float* __restrict__ values, int prior_mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   expand_tree(dp, m, blockIdx.x, logp, values, prior_mode, lds);
+}
+
+// The search half of a simulation plus the next one's descent, per tree, one workgroup of
+// kStepWaves waves: the policy Linear over the leaf's legal ids (all waves: the gather's memory
+// parallelism of k_leaf_logits' 4 x 4 waves), expand/backup (wave 0, prior mode 2), then — when
+// do_select — the next simulation's descent (wave 0) and leaf bitmask / observation (all waves). The same device functions as
+// k_leaf_logits -> k_expand_backup -> k_select, so the trees are bitwise those of the three
+// launches; what goes is two kernel boundaries per simulation and the grid-wide wait for the
+// slowest tree of each stage. Handoffs: this workgroup's global stores visible to its later loads
+// (vmcnt(0), barrier, L1 invalidate).
+__device__ __forceinline__ void wg_store_handoff() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();
+  asm volatile("buffer_inv sc0" ::: "memory");
+}
+#ifndef BK_STEP_WAVES
+#define BK_STEP_WAVES 16  // waves per tree in k_leaf_step: the logit gather's memory parallelism
+#endif
+constexpr int kStepWaves = BK_STEP_WAVES;
+__global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step(DevPreset dp, DevMcts m, const float* __restrict__ feat,
+                                                                 int64_t ldf, int F, const float* __restrict__ W,
+                                                                 const float* __restrict__ bias,
+                                                                 const float* __restrict__ values, int do_select,
+                                                                 const uint32_t* __restrict__ roots,
+                                                                 const int32_t* __restrict__ active, double cpuct,
+                                                                 int32_t* __restrict__ status_out,
+                                                                 float* __restrict__ obs,
+                                                                 uint64_t* __restrict__ mask_out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ int status_sh;
+  const int t = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  leaf_logits_tree<BK_LEAF_R>(dp, m, t, 0, 1, feat, ldf, F, W, bias, lds);
+  wg_store_handoff();
+  if (wave == 0) expand_tree(dp, m, t, nullptr, values, 2, lds);
+  wg_store_handoff();
+  if (!do_select) return;
+  if (wave == 0) {
+    const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lds);
+    if (lane_id() == 0) status_sh = st;
+  }
+  __syncthreads();
+  select_leaf<kStepWaves>(dp, m, t, status_sh, obs, mask_out, lds, wave);
 }
 
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
@@ -240,6 +284,22 @@ int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const
   hipLaunchKernelGGL(k_leaf_logits, dim3(m->d.T, kLeafBlocks), dim3(256), lds, (hipStream_t)stream, dp, m->d, feat,
                      ldf, F, W, bias);
   return launch_check("k_leaf_logits");
+}
+
+int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
+                      const float* values, int do_select, const void* roots, const int32_t* active, double cpuct,
+                      int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream) {
+  BK_REQUIRE(m && feat && W && bias && values && F > 0 && F <= kMaxFeat && ldf >= F, "bad argument");
+  BK_REQUIRE(((uintptr_t)W & 15u) == 0 || (F & 3) != 0, "bk_mcts_leaf_step: W must be 16-byte aligned");
+  BK_REQUIRE(!do_select || (roots && leaf_status && obs), "bad argument: select outputs");
+  const DevPreset& dp = m->ctx->dp;
+  size_t words = (size_t)dp.W32pad + kLeafCap + F;                               // leaf logits
+  words = std::max(words, (size_t)dp.W32pad + kExpandLdsIds);                    // expand
+  words = std::max(words, (size_t)(kStateWords + 2 * kMaxN + dp.W32pad));       // select
+  hipLaunchKernelGGL(k_leaf_step, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
+                     (hipStream_t)stream, dp, m->d, feat, ldf, F, W, bias, values, do_select,
+                     (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask);
+  return launch_check("k_leaf_step");
 }
 
 int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, int prior_mode, void* stream) {

@@ -47,6 +47,8 @@ _SIGS = {
     "bk_mcts_select": (_i, [_vp, _vp, _vp, ctypes.c_double, _vp, _vp, _vp, _vp]),
     "bk_mcts_expand_backup": (_i, [_vp, _vp, _vp, _i, _vp]),
     "bk_mcts_leaf_logits": (_i, [_vp, _vp, ctypes.c_int64, _i, _vp, _vp, _vp]),
+    "bk_mcts_leaf_step": (_i, [_vp, _vp, ctypes.c_int64, _i, _vp, _vp, _vp, _i, _vp, _vp, ctypes.c_double, _vp,
+                               _vp, _vp, _vp]),
     "bk_mcts_simulate_resnet": (_i, [_vp, _vp, _vp, ctypes.c_double, _i, _i] + [_vp] * 21),
     "bk_mcts_simulate_const": (_i, [_vp, _vp, _vp, ctypes.c_double, _i, _vp, _vp, _vp]),
     "bk_mcts_root_policy": (_i, [_vp, _vp, _vp, ctypes.c_double, _vp, _vp, _i, _vp, _vp]),

@@ -162,6 +162,16 @@ int bk_mcts_expand_backup(bk_mcts* m, const float* logp, const float* values, in
 int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
                         void* stream);
 
+/* The search half of a simulation and the descent of the next, in one launch (k_leaf_step, one
+ * workgroup per tree): bk_mcts_leaf_logits(feat, ldf, F, W, bias) -> bk_mcts_expand_backup(NULL,
+ * values, 2) -> (do_select) bk_mcts_select(roots, active, cpuct, leaf_status, obs, leaf_mask),
+ * the same trees bitwise, without the grid-wide step between the three. Replaces, inside the
+ * simulation loop (trainer.py:104-105), the end of one MCTS.simulate (mcts.py:60-70, the priors
+ * of predict, neural_network.py:92-110) and the descent of the next (mcts.py:37-50). */
+int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
+                      const float* values, int do_select, const void* roots, const int32_t* active, double cpuct,
+                      int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream);
+
 /* Whole simulations in one launch (sims.hip, k_sims): for every active tree, nsims x { select ->
  * the leaf ResNet (stem, Winograd residual tower, heads) -> the policy Linear over the leaf's
  * legal ids -> expand/backup (mode 2) }, one workgroup per tree, no grid-wide step between the

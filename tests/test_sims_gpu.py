@@ -51,6 +51,47 @@ def test_fused_simulations_match_stagewise(N, T, sims, monkeypatch):
     assert torch.equal(s1[a], s2[a]) and torch.equal(d1, d2)
 
 
+@pytest.mark.parametrize("N,T,sims", [(20, 12, 9), (14, 7, 6)])
+def test_leaf_step_matches_stagewise(N, T, sims):
+    """bk_mcts_leaf_step (policy head + expand/backup + the next descent in one launch) against
+    k_leaf_logits -> k_expand_backup -> k_select: the same trees, counters, leaf states and
+    observations, bitwise."""
+    from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
+    from blokus_rl_amd.boards import random_boards
+    from blokus_rl_amd.engine import Engine
+
+    eng = Engine(N, 4, 5)
+    model = _leaf_model(eng)
+    roots = random_boards(eng, T, seed0=11, max_plies=24 if N == 20 else 12)
+    active = torch.ones(T, dtype=torch.int32, device=eng.device)
+    active[T // 3] = 0
+    kw = dict(node_cap=64, child_cap=T * 64 * 700)
+    m1, m2 = BatchedMCTS(eng, T, **kw), BatchedMCTS(eng, T, **kw)
+    po = model.f.policy_out
+    w, b = po.weight.detach().contiguous(), po.bias.detach().contiguous()
+    _, obs1, _ = m1.select(roots, active, 1.5)
+    _, obs2, _ = m2.select(roots, active, 1.5)
+    for i in range(sims):
+        pf1, v1 = (t.contiguous() for t in model(obs1))
+        pf2, v2 = (t.contiguous() for t in model(obs2))
+        assert torch.equal(pf1, pf2) and torch.equal(v1, v2)
+        m1.leaf_logits(pf1, w, b)
+        m1.expand_backup(None, v1, 2)
+        last = i == sims - 1
+        if not last:
+            st1, obs1, mk1 = m1.select(roots, active, 1.5)
+        r = m2.leaf_step(pf2, w, b, v2, None if last else roots, active, 1.5)
+        if not last:
+            st2, obs2, mk2 = r
+            assert torch.equal(st1, st2) and torch.equal(obs1, obs2)
+            ok = st1 == 1
+            assert torch.equal(mk1[ok], mk2[ok])
+    c1, c2 = m1.check(), m2.check()
+    assert c1 == c2 and c1["expanded"] > 0
+    for x, y in zip(m1.root_stats(roots, active), m2.root_stats(roots, active)):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("fused,graph", [("1", "1"), ("0", "1")])
 def test_selfplay_plies_match_eager(monkeypatch, fused, graph):
     """The default play_ply paths (fused simulations, or the captured simulation graph) give the
