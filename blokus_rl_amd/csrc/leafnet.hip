@@ -272,8 +272,33 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   LNSTAMP(0, __builtin_amdgcn_s_memtime());
   LNSTAMP(30, __builtin_amdgcn_s_memrealtime());
 
-  // zero both grids (the halo stays zero; interiors are overwritten before they are read)
-  for (int i = tid; i < 18 * PL / 16; i += kLnThreads) reinterpret_cast<u32x4*>(lds)[i] = u32x4{0u, 0u, 0u, 0u};
+  // the observation loads first (their latency under the halo zeroing below)
+  const float* ob = obs + b * kStemCinX3 * NN;
+  float xin[PIX_IT][kStemCinX3];
+#pragma unroll
+  for (int it = 0; it < PIX_IT; ++it) {
+    const int p = tid + it * kLnThreads;
+#pragma unroll
+    for (int c = 0; c < kStemCinX3; ++c) xin[it][c] = p < NN ? ob[c * NN + p] : 0.0f;
+  }
+  // zero the halo of all 18 planes (rows 0 and N+1, columns 0 and N+1..RS-1; the only slots read
+  // that no layer writes: interiors are written before they are read)
+  {
+    constexpr int kHaloCols = RS - N, kHalo = 2 * RS + N * kHaloCols;
+    for (int i = tid; i < 18 * kHalo; i += kLnThreads) {
+      const int plane = i / kHalo, k = i - plane * kHalo;
+      int row, col;
+      if (k < 2 * RS) {
+        row = k < RS ? 0 : N + 1;
+        col = k < RS ? k : k - RS;
+      } else {
+        const int h = k - 2 * RS, c = h % kHaloCols;
+        row = 1 + h / kHaloCols;
+        col = c == 0 ? 0 : N + c;
+      }
+      *reinterpret_cast<u32x4*>(lds + plane * PL + (row * RS + col) * 16) = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
 
   // the lane's grid slot in each group, in bytes (a spare column reads slot 0 of the halo: zeros),
   // and the mask of groups where the lane's column is a board pixel
@@ -315,18 +340,11 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   const f32x4 s_stem = *reinterpret_cast<const f32x4*>(sstem + oc), b_stem = *reinterpret_cast<const f32x4*>(bstem + oc);
 
   // ---- stem input: the planar observation [8][N][N] of the board, scaled by its maximum, split
-  const float* ob = obs + b * kStemCinX3 * NN;
-  float xin[PIX_IT][kStemCinX3];
   float m = 0.0f;
 #pragma unroll
-  for (int it = 0; it < PIX_IT; ++it) {
-    const int p = tid + it * kLnThreads;
+  for (int it = 0; it < PIX_IT; ++it)
 #pragma unroll
-    for (int c = 0; c < kStemCinX3; ++c) {
-      xin[it][c] = p < NN ? ob[c * NN + p] : 0.0f;
-      m = fmaxf(m, fabsf(xin[it][c]));
-    }
-  }
+    for (int c = 0; c < kStemCinX3; ++c) m = fmaxf(m, fabsf(xin[it][c]));
   const float max_obs = block_max(m, red + 8, wave, l);  // the barrier also orders the zeroing before the writes
   int ex = scale_exp(max_obs);
 #pragma unroll
@@ -536,10 +554,13 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       const f32x4* w[3] = {&wp0, &wp1, &wvv};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        float a = y.x * (*w[k]).x + y.y * (*w[k]).y + y.z * (*w[k]).z + y.w * (*w[k]).w;
-        a += __shfl_xor(a, 16);
-        a += __shfl_xor(a, 32);
-        d[k] = a;
+        // the sum over the 4 k-groups: a + a(lane ^ 16), then + (lane ^ 32), as two VALU swaps
+        // (v_permlane16/32_swap) instead of LDS permutes; x + y is the same sum in either order
+        const float a = y.x * (*w[k]).x + y.y * (*w[k]).y + y.z * (*w[k]).z + y.w * (*w[k]).w;
+        const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+        const float a16 = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+        const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a16), __float_as_uint(a16), false, false);
+        d[k] = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
       }
       if (ks == 0 && is_valid(g)) {
         float* dst = hp + (ln_pixel<N>(slot_b(g) / 16) * 4 + wave) * 3;
@@ -565,20 +586,25 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   }
   __syncthreads();
   {
-    const int q0 = (NN * wave) / 4, q1 = (NN * (wave + 1)) / 4;
-    float a0 = 0.f, a1 = 0.f;
-    int i = q0;
-    for (; i + 10 <= q1; i += 10) {
-      float w[10];
+    // wave w: inputs [Q w, Q (w + 1)) of W1 (L2-resident), every load issued before the first FMA
+    constexpr int Q = NN / 4;
+    static_assert(NN % 4 == 0, "k_leafnet_x3: quarters of the value-MLP inputs");
+    const int q0 = Q * wave;
+    float w[Q];
 #pragma unroll
-      for (int u = 0; u < 10; ++u) w[u] = hd.w1t[(size_t)(i + u) * 64 + l];
+    for (int k = 0; k < Q; ++k) w[k] = hd.w1t[(size_t)(q0 + k) * 64 + l];
+    float a0 = 0.f, a1 = 0.f;
+    int k = 0;
+#pragma unroll
+    for (; k + 10 <= Q; k += 10) {
 #pragma unroll
       for (int u = 0; u < 10; u += 2) {
-        a0 += w[u] * vfeat[i + u];
-        a1 += w[u + 1] * vfeat[i + u + 1];
+        a0 += w[k + u] * vfeat[q0 + k + u];
+        a1 += w[k + u + 1] * vfeat[q0 + k + u + 1];
       }
     }
-    for (; i < q1; ++i) a0 += hd.w1t[(size_t)i * 64 + l] * vfeat[i];
+#pragma unroll
+    for (; k < Q; ++k) a0 += w[k] * vfeat[q0 + k];
     part[wave * 64 + l] = a0 + a1;
   }
   __syncthreads();
