@@ -228,7 +228,8 @@ class SelfPlay:
         logp, v, mode = self._evaluate(obs)
         self.mcts.expand_backup(logp, v, prior_mode=mode)
 
-    SIM_GRAPH_SIMS = 10  # simulations per captured graph (paths without a fused kernel)
+    # simulations per captured graph (BK_SIM_GRAPH_SIMS; a ply's n simulations = n // k replays + eager rest)
+    SIM_GRAPH_SIMS = int(os.environ.get("BK_SIM_GRAPH_SIMS", "10"))
 
     def fused(self) -> bool:
         """Whole simulations in one launch (k_sims: the HIP ResNet in fp32 with the sparse policy
