@@ -132,12 +132,15 @@ __device__ __forceinline__ f32x4 mfma16(h16x8 a, h16x8 b, f32x4 c) {
 }
 
 // x (already scaled) -> packed f16 halves: hi = f16(x) (round to nearest), lo = f16(x - hi)
+// (3 VALU ops per pair: x - hi is exact in f32 (|x - hi| <= half an f16 ulp of x), so the mix op's
+// one rounding of fma(-hi, 1, x) to f16 is f16(x - hi) as a convert-back-and-subtract form
+// computes it (5 ops): bitwise the same)
 __device__ __forceinline__ void split2(float x0, float x1, unsigned& hi, unsigned& lo) {
-  const h16x2 h = __builtin_convertvector(f32x2{x0, x1}, h16x2);
-  const f32x2 hf = __builtin_convertvector(h, f32x2);
-  const f32x2 r = f32x2{x0, x1} - hf;
-  hi = __builtin_bit_cast(unsigned, h);
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(r, h16x2));
+  asm("v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+      "v_fma_mixlo_f16 %1, -%0, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%0, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(x0), "v"(x1));
 }
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
@@ -431,9 +434,11 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       // bit_cast the whole vector: hipcc's __builtin_bit_cast of an ext_vector element reads
       // element 0 whatever the index (ROCm 7.2)
       const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);  // {hi 01, hi 23, lo 01, lo 23}
-      const auto r0 = __builtin_amdgcn_permlane16_swap(w.x, w.z, false, false);
-      const auto r1 = __builtin_amdgcn_permlane16_swap(w.y, w.w, false, false);
-      if (is_valid(g)) *reinterpret_cast<u32x4*>(base + slot_b(g)) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+      // the swaps in place (the builtin returns copies: 4 moves per group to rebuild the tuple)
+      unsigned x = w.x, y = w.y, z = w.z, t = w.w;
+      asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3"
+          : "+v"(x), "+v"(z), "+v"(y), "+v"(t));
+      if (is_valid(g)) *reinterpret_cast<u32x4*>(base + slot_b(g)) = u32x4{x, y, z, t};
     }
   };
   // the scale of a conv's output from the bound |y| <= A max_in + B (A = the largest row L1 norm
@@ -485,6 +490,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     // the layer's output scale and bias (folded BN) are loaded here, under the MFMA loop
     const f32x4 sv = *reinterpret_cast<const f32x4*>(st + layer * 64 + oc);
     const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + layer * 64 + oc);
+    // the next conv's output bound (bounds holds the stem and every tower conv: always in range)
+    const float bnd_a = bounds[2 * (layer + 1)], bnd_b = bounds[2 * (layer + 1) + 1];
     // chunk c = (tap c/2, channel half c%2): the lane's octet 4 (c%2) + ks has its hi plane at
     // ks*4 + 2 (c%2) (lo next to it), so from ab the offset is a compile-time immediate < 2^16
     auto coff_of = [&](int c) {
@@ -501,9 +508,12 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       if (cn < 18) {
         wq[sn][0] = wl[cn * 8 * 64];
         wq[sn][1] = wl[cn * 8 * 64 + 64];
-      } else if (more) {  // the next layer's first chunks
-        wq[sn][0] = wl[kLayerBlocks * 64 + (cn - 18) * 8 * 64];
-        wq[sn][1] = wl[kLayerBlocks * 64 + (cn - 18) * 8 * 64 + 64];
+      } else {  // the next layer's first chunks; the last layer reloads its own (never used): an
+                // unconditional load keeps the wait count static (a branch made it vmcnt(0), an
+                // exposed L2 round trip per layer)
+        const size_t nx = more ? (size_t)kLayerBlocks * 64 : 0;
+        wq[sn][0] = wl[nx + (cn - 18) * 8 * 64];
+        wq[sn][1] = wl[nx + (cn - 18) * 8 * 64 + 64];
       }
       const h16x8* w = wq[c % (kLnWpf + 1)];
       if (c == 0)
@@ -515,7 +525,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
     const bool last = layer + 1 == nlayers;
     if (!last) {
-      const int ex_out = out_exp(layer + 1, max_in);
+      const int ex_out = scale_exp(bnd_a * max_in + bnd_b);  // = out_exp(layer + 1, max_in)
       const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
       if (layer == 1) LNSTAMP(21, __builtin_amdgcn_s_memtime());
       post_max(mx, (layer + 1) & 1);
