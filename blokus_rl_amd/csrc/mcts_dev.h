@@ -213,7 +213,7 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
   int depth = 0, err = 0;
   long long scanned = 0;
 #ifdef BK_STAMPS
-  unsigned long long t_probe = 0, t_child = 0, t_apply = 0;
+  unsigned long long t_probe = 0, t_child = 0, t_apply = 0, t_adv = 0;
 #define BK_TACC(v, stmt)                                         \
   do {                                                           \
     const unsigned long long t0_ = __builtin_amdgcn_s_memtime(); \
@@ -240,8 +240,8 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     // the child's action is legal by construction (its id came from the node's legal mask)
     const int p = (int)s[kWToMove];
     int bad;
-    BK_TACC(t_apply, bad = place_action<false>(dp, s, a, fa);
-            if (!bad) advance_turn(dp, s, p, [&](int q) { return rows_any_legal(dp, s, q); }));
+    BK_TACC(t_apply, bad = place_action<false>(dp, s, a, fa));
+    BK_TACC(t_adv, if (!bad) advance_turn(dp, s, p, [&](int q) { return rows_any_legal(dp, s, q); }));
     if (bad) { err |= kErrIllegal; break; }
     if (l == 0) {
       const size_t pi = (size_t)t * kMaxDepth + depth;
@@ -256,7 +256,8 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
   if (lane_id() == 0 && blockIdx.x < 4096) {
     g_stamps[0][blockIdx.x][6] = t_probe;
     g_stamps[0][blockIdx.x][7] = t_child;
-    g_stamps[1][blockIdx.x][7] = t_apply;  // (slot 7 of the expand record is free)
+    g_stamps[1][blockIdx.x][7] = t_apply;  // (slots 6, 7 of the expand record are free)
+    g_stamps[1][blockIdx.x][6] = t_adv;
   }
 #endif
 #undef BK_TACC

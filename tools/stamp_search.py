@@ -35,5 +35,6 @@ for k, names in ((0, ["load", "descent", "build_mask", "mask+state store", "obs 
     for i, n in enumerate(names):
         print(f"   {n:18s} median {int(np.median(d[:, :, i])):8d}  mean {d[:, :, i].mean():10.0f}")
     if k == 0:  # the descent's parts, summed over its levels
-        for n, v in (("  probe", a[:, :, 6]), ("  select_child", a[:, :, 7]), ("  apply_action", np.stack(acc[1])[:, :, 7])):
+        for n, v in (("  probe", a[:, :, 6]), ("  select_child", a[:, :, 7]), ("  place_action", np.stack(acc[1])[:, :, 7]),
+                     ("  advance_turn", np.stack(acc[1])[:, :, 6])):
             print(f"   {n:18s} median {int(np.median(v)):8d}  mean {v.mean():10.0f}")
