@@ -31,9 +31,13 @@ for k, names in ((0, ["load", "descent", "build_mask", "mask+state store", "obs 
     d = np.diff(a[:, :, :6], axis=2)
     tot = a[:, :, 5] - a[:, :, 0]
     print(["k_select", "k_expand_backup"][k], "median total cycles", int(np.median(tot)),
-          "(s_memtime ticks)")
+          "(s_memtime ticks); per launch: mean of the max over trees", int(tot.max(axis=1).mean()),
+          "p90", int(np.percentile(tot, 90)))
     for i, n in enumerate(names):
         print(f"   {n:18s} median {int(np.median(d[:, :, i])):8d}  mean {d[:, :, i].mean():10.0f}")
+    for i, n in enumerate(names):  # the slowest tree of each launch: its phase split
+        sl = np.argmax(tot, axis=1)
+        print(f"   slowest tree {n:14s} mean {np.mean(d[np.arange(len(sl)), sl, i]):10.0f}")
     if k == 0:  # the descent's parts, summed over its levels
         for n, v in (("  probe", a[:, :, 6]), ("  select_child", a[:, :, 7]), ("  place_action", np.stack(acc[1])[:, :, 7]),
                      ("  advance_turn", np.stack(acc[1])[:, :, 6])):
