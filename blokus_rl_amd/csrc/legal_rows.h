@@ -155,11 +155,17 @@ __device__ __forceinline__ bool rows_any_legal(const DevPreset& dp, const uint32
 template <int WPB>
 __device__ __forceinline__ void build_mask_rows_wg(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32,
                                                    int wave) {
+#ifndef BK_MASK_STAMP
+#define BK_MASK_STAMP(i) do { } while (0)
+#endif
   for (int i = threadIdx.x; i < dp.W32pad / 4; i += kWave * WPB)
     reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
   const RowCtx c = row_ctx(dp, s, q, m32);
+  BK_MASK_STAMP(5);
   __syncthreads();
+  BK_MASK_STAMP(6);
   orient_all<WPB, 0>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+  BK_MASK_STAMP(7);
   __syncthreads();
 }
 

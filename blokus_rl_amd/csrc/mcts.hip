@@ -17,6 +17,13 @@
 // The per-tree stages run on one wave (the descent, the expansion) while the other waves of a
 // k_select workgroup wait at a workgroup barrier, so board-level handoffs are wave-scope.
 #define BK_BOARD_SYNC() ::bk::wave_lds_sync()
+#ifdef BK_STAMPS
+#include <hip/hip_runtime.h>
+static __device__ unsigned long long g_step_stamps[4096][8];  // diag: k_leaf_step phase stamps
+// diag: phases inside the leaf bitmask build of k_leaf_step (slots 5..7), thread 0 of the group
+#define BK_MASK_STAMP(i) \
+  do { if (threadIdx.x == 0 && blockIdx.x < 4096 && blockDim.x > 256) g_step_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#endif
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -103,17 +110,29 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step(DevPreset dp, Dev
   __shared__ int status_sh;
   const int t = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef BK_STAMPS
+#define BK_STEP_STAMP(i) \
+  do { if (do_select && threadIdx.x == 0 && t < 4096) g_step_stamps[t][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BK_STEP_STAMP(i) do { } while (0)
+#endif
+  BK_STEP_STAMP(0);
   leaf_logits_tree<BK_LEAF_R>(dp, m, t, 0, 1, feat, ldf, F, W, bias, lds);
   wg_store_handoff();
+  BK_STEP_STAMP(1);
   if (wave == 0) expand_tree(dp, m, t, nullptr, values, 2, lds);
   wg_store_handoff();
+  BK_STEP_STAMP(2);
   if (!do_select) return;
   if (wave == 0) {
     const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lds);
     if (lane_id() == 0) status_sh = st;
   }
   __syncthreads();
+  BK_STEP_STAMP(3);
   select_leaf<kStepWaves>(dp, m, t, status_sh, obs, mask_out, lds, wave);
+  BK_STEP_STAMP(4);
+#undef BK_STEP_STAMP
 }
 
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
@@ -201,6 +220,9 @@ extern "C" {
 #ifdef BK_STAMPS
 int bk_debug_stamps(unsigned long long* out) {  // [2][4096][8] host copy
   return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)), "stamps");
+}
+int bk_debug_step_stamps(unsigned long long* out) {  // [4096][8] host copy: k_leaf_step phases
+  return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamps), sizeof(g_step_stamps)), "step stamps");
 }
 #endif
 

@@ -134,6 +134,9 @@ __device__ __forceinline__ void wave_argmax(double& best, int& bi) {
 // memory round trip: each lane loads all its children's (P, N, Q, id) first, the visit sum is
 // the wave's integer sum of N, then the lane scans its children in index order.
 constexpr int kSelB = 12;
+#ifndef BK_MASK_WPB
+#define BK_MASK_WPB 16  // A/B knob: waves that take orientations in a leaf bitmask (the rest idle)
+#endif
 __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, double cp, int& id_out) {
   const int l = lane_id();
   double best = -INFINITY;
@@ -298,7 +301,7 @@ __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& 
     if (NW == 1)
       build_mask_rows(dp, s, (int)s[kWToMove], m32);
     else
-      build_mask_rows_wg<NW>(dp, s, (int)s[kWToMove], m32, wave);
+      build_mask_rows_wg<(NW > BK_MASK_WPB ? BK_MASK_WPB : NW)>(dp, s, (int)s[kWToMove], m32, wave);
     BK_STAMP(0, 3);
     uint64_t* mo = m.leaf_mask + (size_t)t * dp.W64;
     uint64_t* mo2 = mask_out ? mask_out + (size_t)t * dp.W64 : nullptr;
