@@ -263,6 +263,8 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
   if (!rc) rc = mcts_alloc(m, &d.leaf_K, T);
   if (!rc) rc = mcts_alloc(m, &d.counters, 8);
   if (!rc) rc = hip_check(hipMemset(d.counters, 0, 8 * sizeof(unsigned long long)), "memset counters");
+  if (!rc) rc = mcts_alloc(m, &d.tree_ctr, T * 8);
+  if (!rc) rc = hip_check(hipMemset(d.tree_ctr, 0, T * 8 * sizeof(unsigned long long)), "memset tree counters");
   if (!rc) rc = hip_check(hipMemset(d.leaf_status, 0, T * sizeof(int32_t)), "memset status");
   if (!rc) rc = hip_check(hipMemset(d.depth, 0, T * sizeof(int32_t)), "memset depth");
   if (rc) { bk_mcts_destroy(m); return rc; }
@@ -374,8 +376,16 @@ int bk_mcts_counters(bk_mcts* m, int64_t* out, void* stream) {
   if (!rc) rc = hip_check(hipMemcpy(ch.data(), m->d.tree_children, sizeof(int64_t) * m->d.T,
                                     hipMemcpyDeviceToHost), "copy children");
   if (rc) return rc;
+  std::vector<unsigned long long> tcs((size_t)m->d.T * 8);
+  rc = hip_check(hipMemcpy(tcs.data(), m->d.tree_ctr, sizeof(unsigned long long) * tcs.size(), hipMemcpyDeviceToHost),
+                 "copy tree counters");
+  if (rc) return rc;
   int64_t tn = 0, tc = 0;
-  for (int t = 0; t < m->d.T; ++t) { tn += nodes[t]; tc += ch[t]; }
+  for (int t = 0; t < m->d.T; ++t) {
+    tn += nodes[t];
+    tc += ch[t];
+    for (int k = 2; k < 8; ++k) c[k] += tcs[(size_t)t * 8 + k];  // per-tree parts (k_err stays global)
+  }
   out[0] = tn;
   out[1] = tc;
   for (int k = 2; k < 8; ++k) out[k] = (int64_t)c[k];

@@ -63,8 +63,22 @@ struct DevMcts {
   int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
   float* leaf_logit;    // [T*kLeafCap] their logits
   int32_t* leaf_K;      // [T]
-  unsigned long long* counters;  // [8]
+  unsigned long long* counters;  // [8] (errors; the totals when BK_TREE_CTR is 0)
+  unsigned long long* tree_ctr;  // [T*8] per-tree counters: uncontended atomics, summed on read
 };
+
+#ifndef BK_TREE_CTR
+#define BK_TREE_CTR 1  // A/B knob: per-tree counters (1) or one contended set for all trees (0)
+#endif
+// add v to counter k of tree t: fire-and-forget, on an address no other tree touches (every
+// tree on one shared counter serialised 256 atomics per stage in L2, which the workgroup's next
+// barrier then waited for)
+__device__ __forceinline__ void ctr_add(const struct DevMcts& m, int t, int k, unsigned long long v) {
+  if (BK_TREE_CTR)
+    atomicAdd(&m.tree_ctr[(size_t)t * 8 + k], v);
+  else
+    atomicAdd(&m.counters[k], v);
+}
 
 enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5, kCtrScanned = 6, kCtrLeafK = 7 };
 enum { kErrChildPool = 1, kErrTable = 2, kErrDepth = 4, kErrIllegal = 8, kErrMissingRoot = 16, kErrLeafCap = 32 };
@@ -277,9 +291,9 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     m.leaf_status[t] = status;
     if (status_out) status_out[t] = status;
     m.depth[t] = depth;
-    atomicAdd(&m.counters[kCtrLevels], (unsigned long long)depth);
-    atomicAdd(&m.counters[kCtrScanned], (unsigned long long)scanned);
-    if (status == 2) atomicAdd(&m.counters[kCtrTerminal], 1ull);
+    ctr_add(m, t, kCtrLevels, (unsigned long long)depth);
+    ctr_add(m, t, kCtrScanned, (unsigned long long)scanned);
+    if (status == 2) ctr_add(m, t, kCtrTerminal, 1ull);
     if (err) atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
   }
   return status;
@@ -607,8 +621,8 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
         m.tab[(size_t)t * m.TS + free_slot] = e;
         m.tree_nodes[t] = node + 1;
         m.tree_children[t] = used + K;
-        atomicAdd(&m.counters[kCtrExpanded], 1ull);
-        atomicAdd(&m.counters[kCtrLeafK], (unsigned long long)K);
+        ctr_add(m, t, kCtrExpanded, 1ull);
+        ctr_add(m, t, kCtrLeafK, (unsigned long long)K);
       }
     } else if (l == 0) {
       atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
