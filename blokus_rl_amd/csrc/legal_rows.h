@@ -33,6 +33,12 @@ struct RowCtx {
 #ifdef BK_NOATOMIC  // timing experiment only (wrong masks): plain stores instead of LDS atomics
 #define atomicOr(p, v) (*(p) = (v))
 #endif
+#ifndef BK_MASK_SPLIT
+#define BK_MASK_SPLIT 0  // A/B knob: even / odd origin rows in separate LDS atomics (leaf bitmask)
+#endif
+#ifndef BK_MASK_DIRECT
+#define BK_MASK_DIRECT 1  // A/B knob: each wave runs only its orientations (orient_dispatch)
+#endif
 template <int O, int WPB, int SPLIT>
 __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c, int wave, int& base) {
   constexpr OrientC oc = kOrient[O];
@@ -79,6 +85,47 @@ __device__ __forceinline__ void orient_all(const DevPreset& dp, const RowCtx& c,
                                            std::index_sequence<Os...>) {
   int base = 0;
   (orient_step<(int)Os, WPB, SPLIT>(dp, c, wave, base), ...);
+}
+
+// The bit offset of orientation O's fields in the mask, base(O) = sum over O' < O of
+// (N - h' + 1)(N - w' + 1) = cnt N^2 + b N + c with compile-time prefix sums (the orientations
+// of the pieces a preset uses are a prefix of the table, sorted by piece).
+struct OrientBase {
+  int cnt[kNumOrient + 1], b[kNumOrient + 1], c[kNumOrient + 1];
+};
+constexpr OrientBase make_orient_base() {
+  OrientBase t{};
+  for (int i = 0; i < kNumOrient; ++i) {
+    t.cnt[i + 1] = t.cnt[i] + 1;
+    t.b[i + 1] = t.b[i] + (2 - kOrient[i].h - kOrient[i].w);
+    t.c[i + 1] = t.c[i] + (1 - kOrient[i].h) * (1 - kOrient[i].w);
+  }
+  return t;
+}
+constexpr OrientBase kOrientBase = make_orient_base();
+
+// Wave W of WPB's orientations (O = W, W + WPB, ...) straight: no steps over the other waves'
+// orientations (stepping over 85 of 91 unrolled orientations per wave, each a scalar branch and
+// the base update, took ~14k cycles per leaf bitmask at 16 waves: the walk, not the work)
+template <int O>
+__device__ __forceinline__ void orient_step_at(const DevPreset& dp, const RowCtx& c) {
+  constexpr OrientC oc = kOrient[O];
+  if (oc.piece >= dp.num_pieces) return;  // wave-uniform
+  const int N = dp.N;
+  int base = kOrientBase.cnt[O] * N * N + kOrientBase.b[O] * N + kOrientBase.c[O];
+  orient_step<O, 1, BK_MASK_SPLIT>(dp, c, 0, base);
+}
+template <int W, int WPB, size_t... Ks>
+__device__ __forceinline__ void orient_part(const DevPreset& dp, const RowCtx& c, std::index_sequence<Ks...>) {
+  (orient_step_at<W + (int)Ks * WPB>(dp, c), ...);
+}
+template <int WPB, size_t... Ws>
+__device__ __forceinline__ void orient_dispatch(const DevPreset& dp, const RowCtx& c, int wave,
+                                                std::index_sequence<Ws...>) {
+  // wave-uniform: each wave runs only its own instance
+  ((wave == (int)Ws ? orient_part<(int)Ws, WPB>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
+                    : void()),
+   ...);
 }
 
 // The row context of colour q on the board s (LDS) for lanes 0..N-1 (the board's rows); lanes
@@ -164,7 +211,11 @@ __device__ __forceinline__ void build_mask_rows_wg(const DevPreset& dp, const ui
   BK_MASK_STAMP(5);
   __syncthreads();
   BK_MASK_STAMP(6);
+#if BK_MASK_DIRECT
+  orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
+#else
   orient_all<WPB, 0>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+#endif
   BK_MASK_STAMP(7);
   __syncthreads();
 }

@@ -32,6 +32,8 @@ m = buf[:256, :8].astype(np.int64)
 for n, (i, j) in (("descent end -> ctx done (zero, row_ctx)", (3, 5)), ("first barrier", (5, 6)),
                   ("orientations (thread 0's wave)", (6, 7)), ("second barrier .. obs end", (7, 4))):
     print(f"  mask: {n:40s} median {int(np.median(m[:, j] - m[:, i])):8d}")
+if "--twice" in sys.argv:
+    print(f"  mask: orientations again (warm)  median {int(np.median(m[:, 3] - m[:, 7])):8d}")
 # the select side of the same launch (select_descend / select_leaf stamps, g_stamps[0])
 lib.bk_debug_stamps.argtypes = [ctypes.c_void_p]
 sb = np.zeros((2, 4096, 8), dtype=np.uint64)
