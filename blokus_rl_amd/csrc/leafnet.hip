@@ -64,6 +64,9 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 // a chunk load the first kLnPf of the next), so the LDS latency is never exposed at a chunk start.
 // The slot of group g is g % kLnSlots in every chunk, which needs NG % kLnSlots == 0: the board's
 // groups are padded with spare ones (all columns spare: halo reads, no writes) up to a multiple.
+#ifndef BK_LN_WBUF
+#define BK_LN_WBUF 1  // A/B knob: tower weights through buffer loads (SGPR chunk offsets)
+#endif
 #ifndef BK_LN_PF
 #define BK_LN_PF 2  // groups of read-ahead (A/B knob, 1..4)
 #endif
@@ -164,6 +167,16 @@ __device__ __forceinline__ float max3_abs(float m, float a, float b) {
 // one v_max_i32 (the float max would add a canonicalize per input)
 __device__ __forceinline__ float max_bits(float y, int floor) {
   return __builtin_bit_cast(float, max(__builtin_bit_cast(int, y), floor));
+}
+
+// a buffer resource over [p, p + bytes), its base made provably wave-uniform (readfirstlane): the
+// tower's weight loads as buffer ops (a per-lane VGPR offset + a wave-uniform SGPR offset per
+// chunk) instead of one 64-bit VGPR address per load
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ln_rsrc(const void* p, unsigned bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  const uintptr_t u = ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, (int)bytes, 0x00020000);
 }
 
 // the power of two that brings the largest magnitude m into [2^14, 2^15)
@@ -324,14 +337,24 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // on into the next layer (18 chunks per layer: the ring slot of chunk c is c % (kLnWpf + 1) in
   // every layer), so no layer starts on an exposed L2 load
   static_assert(18 % (kLnWpf + 1) == 0, "BK_LN_WPF: the ring must divide the 18 chunks of a layer");
+  constexpr int kLayerBlocks = 18 * 4 * 2;  // (chunk, wave, part) blocks of 64 x 16 B per layer
+#if BK_LN_WBUF
+  const __amdgpu_buffer_rsrc_t wrs = ln_rsrc(wt, (unsigned)nlayers * kLayerBlocks * 1024u);
+  // part p (0 hi, 1 lo) of the lane's A fragment of chunk c of tower layer `layer`
+  auto wload = [&](int layer, int c, int p) {
+    return __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                         wrs, l * 16, ((layer * kLayerBlocks + c * 8 + wave * 2 + p) * 64) * 16, 0));
+  };
+#else
+  auto wload = [&](int layer, int c, int p) {
+    return wt[(size_t)layer * kLayerBlocks * 64 + (size_t)(c * 8 + wave * 2 + p) * 64 + l];
+  };
+#endif
   h16x8 wq[kLnWpf + 1][2];  // issued here: in flight under the stem
-  {
-    const h16x8* w0 = wt + (wave * 2) * 64 + l;
 #pragma unroll
-    for (int c = 0; c < kLnWpf; ++c) {
-      wq[c][0] = w0[c * 8 * 64];
-      wq[c][1] = w0[c * 8 * 64 + 64];
-    }
+  for (int c = 0; c < kLnWpf; ++c) {
+    wq[c][0] = wload(0, c, 0);
+    wq[c][1] = wload(0, c, 1);
   }
   // the stem's weights (3 chunks), scale and bias, in flight under the observation loads
   h16x8 wsa[3][2];
@@ -483,9 +506,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 
   // ---- residual tower: nlayers convs 64 -> 64; ReLU after each block's first conv; the last
   // adds x0 and takes the ReLU (x = relu(x + res_blocks(x)), blokus_nnet.py:140-141)
-  constexpr int kLayerBlocks = 18 * 4 * 2;  // (chunk, wave, part) blocks per layer
   for (int layer = 0; layer < nlayers; ++layer) {
-    const h16x8* wl = wt + (size_t)layer * kLayerBlocks * 64 + (wave * 2) * 64 + l;
     const bool more = layer + 1 < nlayers;
     // the layer's output scale and bias (folded BN) are loaded here, under the MFMA loop
     const f32x4 sv = *reinterpret_cast<const f32x4*>(st + layer * 64 + oc);
@@ -506,14 +527,14 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       if (layer == 1 && c == 9) LNSTAMP(28, __builtin_amdgcn_s_memtime());
       const int cn = c + kLnWpf, sn = cn % (kLnWpf + 1);
       if (cn < 18) {
-        wq[sn][0] = wl[cn * 8 * 64];
-        wq[sn][1] = wl[cn * 8 * 64 + 64];
+        wq[sn][0] = wload(layer, cn, 0);
+        wq[sn][1] = wload(layer, cn, 1);
       } else {  // the next layer's first chunks; the last layer reloads its own (never used): an
                 // unconditional load keeps the wait count static (a branch made it vmcnt(0), an
                 // exposed L2 round trip per layer)
-        const size_t nx = more ? (size_t)kLayerBlocks * 64 : 0;
-        wq[sn][0] = wl[nx + (cn - 18) * 8 * 64];
-        wq[sn][1] = wl[nx + (cn - 18) * 8 * 64 + 64];
+        const int nl = more ? layer + 1 : layer;
+        wq[sn][0] = wload(nl, cn - 18, 0);
+        wq[sn][1] = wload(nl, cn - 18, 1);
       }
       const h16x8* w = wq[c % (kLnWpf + 1)];
       if (c == 0)
