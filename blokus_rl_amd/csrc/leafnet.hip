@@ -64,6 +64,12 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 // a chunk load the first kLnPf of the next), so the LDS latency is never exposed at a chunk start.
 // The slot of group g is g % kLnSlots in every chunk, which needs NG % kLnSlots == 0: the board's
 // groups are padded with spare ones (all columns spare: halo reads, no writes) up to a multiple.
+#ifndef BK_LN_X0A
+#define BK_LN_X0A 1  // A/B knob: the stem output x0 in AGPRs through the tower
+#endif
+#ifndef BK_LN_WRITE8
+#define BK_LN_WRITE8 1  // A/B knob: activation stores as two 8-B stores per lane (no lane swaps)
+#endif
 #ifndef BK_LN_WBUF
 #define BK_LN_WBUF 1  // A/B knob: tower weights through buffer loads (SGPR chunk offsets)
 #endif
@@ -451,6 +457,19 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // both lo halves, so each lane stores one 16-B slot (hi plane, or the lo plane next to it).
   auto write_act = [&]() {
     const int o = 2 * wave + (ks >> 1);
+#if BK_LN_WRITE8
+    // each lane stores its 4 channels' hi and lo halves (8 B each) into its half of the octet's
+    // 16-B slot in the hi plane and in the lo plane (no lane swaps)
+    unsigned char* base = act + ((o & 3) * 4 + (o >> 2) * 2) * PL + (ks & 1) * 8;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);  // {hi 01, hi 23, lo 01, lo 23}
+      if (is_valid(g)) {
+        *reinterpret_cast<u32x2*>(base + slot_b(g)) = u32x2{w.x, w.y};
+        *reinterpret_cast<u32x2*>(base + slot_b(g) + PL) = u32x2{w.z, w.w};
+      }
+    }
+#else
     unsigned char* base = act + ((o & 3) * 4 + (o >> 2) * 2 + (ks & 1)) * PL;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -463,6 +482,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
           : "+v"(x), "+v"(z), "+v"(y), "+v"(t));
       if (is_valid(g)) *reinterpret_cast<u32x4*>(base + slot_b(g)) = u32x4{x, y, z, t};
     }
+#endif
   };
   // the scale of a conv's output from the bound |y| <= A max_in + B (A = the largest row L1 norm
   // of the weights, B = the largest |bias|: nets.pack_x3)
@@ -495,6 +515,11 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
                      __builtin_bit_cast(float, l1)};
     }
+#if BK_LN_X0A
+    // x0 waits out the tower in AGPRs (read once, by the last conv): its VGPRs go to the loop
+#pragma unroll
+    for (int g = 0; g < NG; ++g) asm volatile("" : "+a"(x0[g]));
+#endif
     post_max(mx, 0);
     __syncthreads();  // the stem's input planes are a separate region: nothing else to wait for
     write_act();
