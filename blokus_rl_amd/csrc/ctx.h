@@ -14,7 +14,7 @@ struct bk_ctx {
   uint64_t* d_items = nullptr;
   uint32_t* d_act = nullptr;
   bool legal_items_kernel = false;  // BK_LEGAL_KERNEL=items selects the item-loop kernel (A/B)
-  int legal_wpb = 11;               // BK_LEGAL_WPB: variant of k_legal_mask_rows (A/B knob)
+  int legal_wpb = 1;                // BK_LEGAL_WPB: variant of k_legal_mask_rows (A/B knob)
 };
 
 namespace bk {

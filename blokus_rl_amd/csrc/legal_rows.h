@@ -21,6 +21,7 @@ struct RowCtx {
   uint32_t ar[5];      // bit-reversed anchor rows r..r+4
   uint32_t rowok[6];   // rowok[h] = ~0 when a placement of height h fits below row r (and the lane is real)
   uint32_t pieces;     // unused pieces of the mover
+  uint32_t upieces;    // wave-uniform: the pieces some board of the wave still has (skip the rest)
   int rN1;             // r * (N + 1): bit offset of origin row r is base + r*(N+1) - r*w
   int r;
   uint32_t* mb;        // this lane's board bitmask in LDS
@@ -45,7 +46,9 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
   if (oc.piece >= dp.num_pieces) return;  // wave-uniform (presets use a prefix of the pieces)
   const int W = dp.N - oc.w + 1;
   const int R = dp.N - oc.h + 1;
-  if (WPB > 1 && (O % WPB) != wave) {  // another wave of the workgroup owns this orientation
+  // another wave of the workgroup owns this orientation, or no board of the wave has its piece
+  // (scalar test; the bits stay as zeroed)
+  if ((WPB > 1 && (O % WPB) != wave) || !((c.upieces >> oc.piece) & 1u)) {
     base += R * W;
     return;
   }
@@ -69,9 +72,9 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
       atomicOr(dst, (uint32_t)x);
       atomicOr(dst + 1, (uint32_t)(x >> 32));
     }
-    if (c.r & 1) {
-      atomicOr(dst, (uint32_t)x);
+    if (c.r & 1) {  // the other word first: otherwise the compiler merges the two branches
       atomicOr(dst + 1, (uint32_t)(x >> 32));
+      atomicOr(dst, (uint32_t)x);
     }
   } else {
     atomicOr(dst, (uint32_t)x);
@@ -160,6 +163,7 @@ __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s
   c.r = r;
   c.rN1 = r * (N + 1);
   c.pieces = s[kWPieces + q];
+  c.upieces = __builtin_amdgcn_readfirstlane(c.pieces);
 #pragma unroll
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32;
@@ -175,7 +179,7 @@ __device__ __forceinline__ bool orient_any(const DevPreset& dp, const RowCtx& c,
   auto step = [&](auto oi) {
     constexpr int O = decltype(oi)::value;
     constexpr OrientC oc = kOrient[O];
-    if (found || oc.piece >= dp.num_pieces || !((c.pieces >> oc.piece) & 1u)) return;  // wave-uniform
+    if (found || oc.piece >= dp.num_pieces || !((c.upieces >> oc.piece) & 1u)) return;  // wave-uniform
     uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
     uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
 #pragma unroll
@@ -254,6 +258,7 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
   c.r = r;
   c.rN1 = r * (N + 1);
   c.pieces = s[kWPieces + q];
+  c.upieces = __builtin_amdgcn_readfirstlane(c.pieces);
 #pragma unroll
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32;
@@ -329,11 +334,24 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   c.r = r;
   c.rN1 = r * (N + 1);
   c.pieces = pieces;
+  // no piece skip here: with 3 boards per wave a piece absent from all three is rare, and the
+  // branches cost the compiler its sharing of the shifted rows across orientations (+50% VALU)
+  c.upieces = ~0u;
 #pragma unroll
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32 + (j < bpw ? j : 0) * dp.W32pad;
   __syncthreads();  // mask zeroing complete
+#if BK_MASK_DIRECT
+  if constexpr (WPB > 1) {
+    // each wave only its own orientations at compile-time bases: orient_all's walk over the
+    // other waves' orientations (a scalar branch + base update each) doubled the instruction count
+    orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
+  } else {
+    orient_all<WPB, SPLIT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+  }
+#else
   orient_all<WPB, SPLIT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+#endif
   __syncthreads();
   // stream out every board of the group: 16-B stores when rows are 16-B aligned (W64 even);
   // popcounts accumulate per lane, one wave reduction and one LDS add per board
