@@ -227,6 +227,39 @@ int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int devi
                                     hipMemcpyHostToDevice), "copy items");
   if (!rc) rc = hip_check(hipMemcpy(c->d_act, p.act.data(), sizeof(uint32_t) * p.act.size(),
                                     hipMemcpyHostToDevice), "copy act");
+  if (!rc) {
+    // k_legal_mask_staged's pack table: u32 word k of the mask is the OR over the fields
+    // overlapping it of hi32(field << sh), field (O, r) at stage slot O * kStageRows + r starting
+    // at bit S = base(O) + r * W, sh = S - 32k + 32; entries 18 bits (slot | sh << 12), 3 per u64.
+    // Presets whose narrowest field is short enough that a word can overlap > 3 fields (N < 20)
+    // have no table: the staged variant falls back to the atomic kernel there.
+    std::vector<uint64_t> ent(2 * (size_t)p.mask_words, 0ull);
+    std::vector<int> used(2 * (size_t)p.mask_words, 0);
+    int64_t base = 0;
+    bool fits = true;
+    for (size_t o = 0; o < p.orients.size() && fits; ++o) {
+      const int h = p.orients[o][1], w = p.orients[o][2];
+      const int R = p.N - h + 1, W = p.N - w + 1;
+      for (int r = 0; r < R && fits; ++r) {
+        const int64_t S = base + (int64_t)r * W;
+        for (int64_t k = S / 32; k <= (S + W - 1) / 32; ++k) {
+          const int sh = (int)(S - 32 * k + 32);
+          const int64_t slot = (int64_t)o * kStageRows + r;
+          if (k >= (int64_t)ent.size() || used[k] >= 3 || sh < 1 || sh > 63 || slot >= 4096) {
+            fits = false;
+            break;
+          }
+          ent[k] |= ((uint64_t)slot | ((uint64_t)sh << 12)) << (18 * used[k]++);
+        }
+      }
+      base += (int64_t)R * W;
+    }
+    if (fits && base == p.A) {
+      rc = hip_check(hipMalloc(&c->d_pack, sizeof(uint64_t) * ent.size()), "hipMalloc pack");
+      if (!rc) rc = hip_check(hipMemcpy(c->d_pack, ent.data(), sizeof(uint64_t) * ent.size(), hipMemcpyHostToDevice),
+                              "copy pack");
+    }
+  }
   if (rc) { bk_ctx_destroy(c); return rc; }
   d.items = c->d_items;
   d.act = c->d_act;
@@ -238,6 +271,7 @@ int bk_ctx_destroy(bk_ctx* c) {
   if (!c) return BK_OK;
   if (c->d_items) (void)hipFree(c->d_items);
   if (c->d_act) (void)hipFree(c->d_act);
+  if (c->d_pack) (void)hipFree(c->d_pack);
   delete c;
   return BK_OK;
 }
@@ -299,6 +333,15 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
       }
       BK_LEGAL_LAUNCH(1, 0);
       break;
+    case 31: {  // staged: no LDS atomics (legal_rows.h)
+      if (!c->d_pack || kWave / c->dp.N > kStageMaxBoards) { BK_LEGAL_LAUNCH(1, 0); break; }
+      const int bytes = legal_stage_lds_bytes(c->dp.N);
+      static const void* fns[] = {(const void*)k_legal_mask_staged<kStageMaxBoards>};
+      if (int rc = set_max_dynamic_lds(fns, 1, bytes)) return rc;
+      hipLaunchKernelGGL(k_legal_mask_staged<kStageMaxBoards>, grid, dim3(64), bytes, st, c->dp, sp, players, B,
+                         (const uint4*)c->d_pack, mask_words, counts);
+      return launch_check("k_legal_mask_staged");
+    }
     case 11: BK_LEGAL_LAUNCH(1, 1); break;  // even/odd origin rows in separate LDS atomics: 15.1 vs 12.1 us
     default: BK_LEGAL_LAUNCH(1, 0); break;  // 1: one wave per group of 3 boards (the default)
   }

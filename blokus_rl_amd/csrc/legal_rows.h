@@ -381,4 +381,158 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   if (counts && threadIdx.x < nb) counts[b0 + threadIdx.x] = cnt_sh[threadIdx.x];
 }
 
+// ---- staged form (BK_LEGAL_WPB=31): no LDS atomics ----
+// The mask is the concatenation, in (orientation, origin row) order, of every row's W-bit field
+// of legal origin columns. The atomic form ORs each field into its (one or two) words: 182 LDS
+// atomics per wave, same-word lanes serialised (PMC: 72% of the LDS cycles were conflicts). Here
+// each lane stores its field whole, one conflict-free ds_write_b32 per orientation at a slot
+// (orientation, row) of its board's stage, and the words are then assembled from a host-built
+// pack table: output u32 word k is the OR of at most three fields, entry = (slot, sh) with
+// contribution hi32(field << sh) (sh = start bit - 32k + 32; an empty entry has sh = 0 -> 0).
+constexpr int kStageRows = kMaxN + 4;  // rows kMaxN.. are spare slots for the lanes past the boards
+constexpr int kStageWords = kNumOrient * kStageRows;
+constexpr int kStageMaxBoards = 9;     // floor(64 / 7)
+constexpr int kPackPrefetch = 8;       // table entries per lane held in registers (W64 <= 512 at N=20)
+__host__ __device__ constexpr int legal_stage_lds_bytes(int N) {
+  return 4 * ((kWave / N + (kWave - (kWave / N) * N > kStageRows - kMaxN ? 1 : 0)) * kStageWords + kWave);
+}
+
+template <int O>
+__device__ __forceinline__ void orient_stage(const DevPreset& dp, const RowCtx& c) {
+  constexpr OrientC oc = kOrient[O];
+  if (oc.piece >= dp.num_pieces) return;  // wave-uniform (not in the mask)
+  const int W = dp.N - oc.w + 1;
+  uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
+  uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
+#pragma unroll
+  for (int k = 1; k < oc.n; ++k) {
+    bad |= c.fr[oc.dr[k]] << oc.dc[k];
+    good |= c.ar[oc.dr[k]] << oc.dc[k];
+  }
+  const uint32_t colmask = (1u << W) - 1u;
+  const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
+  c.mb[O * kStageRows] = __brev(good & ~bad) & colmask & c.rowok[oc.h] & pmask;  // immediate offset
+}
+template <size_t... Os>
+__device__ __forceinline__ void orient_stage_all(const DevPreset& dp, const RowCtx& c, std::index_sequence<Os...>) {
+  (orient_stage<(int)Os>(dp, c), ...);
+}
+__device__ __forceinline__ uint32_t pack_word(uint64_t e, const uint32_t* st) {
+  uint32_t w = 0u;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t ent = (uint32_t)(e >> (18 * i)) & 0x3FFFFu;
+    const uint64_t f = (uint64_t)st[ent & 0xFFFu] << (ent >> 12);
+    w |= (uint32_t)(f >> 32);
+  }
+  return w;
+}
+
+// One wave per group of floor(64/N) boards (lanes = board rows, as k_legal_mask_rows).
+// LDS: legal_stage_lds_bytes(). pack: [W64] x uint4 (the entries of words 2p, 2p+1).
+template <int MaxBoards>  // kStageMaxBoards (a template so the header's kernel links once)
+__global__ __launch_bounds__(64) void k_legal_mask_staged(DevPreset dp, const uint32_t* __restrict__ states,
+                                                          const int32_t* __restrict__ players, int B,
+                                                          const uint4* __restrict__ pack,
+                                                          uint64_t* __restrict__ masks,
+                                                          int32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t st32[];
+  const int l = lane_id();
+  const int N = dp.N;
+  const int bpw = kWave / N;
+  const int j = l / N;
+  const int r = l - j * N;
+  const int b0 = blockIdx.x * bpw;
+  const int b = b0 + j;
+  const bool ok = j < bpw && b < B;
+  uint32_t o0 = 0u, o1 = 0u, o2 = 0u, o3 = 0u, pieces4[kMaxP] = {0u, 0u, 0u, 0u};
+  int q = 0;
+  if (ok) {
+    const uint32_t* s = states + (size_t)b * kStateWords;
+    o0 = s[r];
+    o1 = s[kMaxN + r];
+    o2 = s[2 * kMaxN + r];
+    o3 = s[3 * kMaxN + r];
+#pragma unroll
+    for (int k = 0; k < kMaxP; ++k) pieces4[k] = s[kWPieces + k];
+    q = players ? players[b] : -1;
+    if (q < 0) q = (int)s[kWToMove];
+  }
+  // the pack table's entries of this lane's words, loaded now: they arrive under the
+  // orientation work (a dependent table load per word in the pack loop cost ~3 us per launch)
+  uint4 pe[kPackPrefetch];
+#pragma unroll
+  for (int i = 0; i < kPackPrefetch; ++i)
+    pe[i] = l + i * kWave < dp.W64 ? pack[l + i * kWave] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t own = q == 0 ? o0 : q == 1 ? o1 : q == 2 ? o2 : o3;
+  const uint32_t pieces = q == 0 ? pieces4[0] : q == 1 ? pieces4[1] : q == 2 ? pieces4[2] : pieces4[3];
+  const uint32_t occ = o0 | o1 | o2 | o3;
+  const uint32_t up_raw = __shfl(own, l - 1 < 0 ? 0 : l - 1, kWave);
+  const uint32_t dn_raw = __shfl(own, l + 1 > kWave - 1 ? kWave - 1 : l + 1, kWave);
+  const uint32_t up = r > 0 ? up_raw : 0u;
+  const uint32_t dn = r + 1 < N ? dn_raw : 0u;
+  const uint64_t owners = __ballot(ok && own != 0u);
+  const uint64_t rows_of_board = (N >= 64 ? ~0ull : ((1ull << N) - 1ull)) << (j * N);
+  const bool first = (owners & rows_of_board) == 0ull;
+  uint32_t forb = 0u, anch = 0u;
+  if (ok) {
+    forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
+    if (first)
+      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+    else
+      anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
+  }
+  RowCtx c;
+  c.fr[0] = __brev(forb);
+  c.ar[0] = __brev(anch);
+#pragma unroll
+  for (int d = 1; d < 5; ++d) {
+    const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
+    c.fr[d] = __shfl(c.fr[0], src, kWave);
+    c.ar[d] = __shfl(c.ar[0], src, kWave);
+  }
+  c.r = r;
+  c.rN1 = r * (N + 1);
+  c.pieces = pieces;
+  c.upieces = ~0u;
+#pragma unroll
+  for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
+  // the lanes past the last board (their fields are 0) store into board 0's spare rows, or into
+  // a scratch stage after the boards when there are more of them than spare rows (never packed)
+  const int idle = l - bpw * N;
+  c.mb = j < bpw ? st32 + j * kStageWords + r
+                 : (kWave - bpw * N <= kStageRows - kMaxN ? st32 + kMaxN + idle : st32 + bpw * kStageWords + idle);
+  orient_stage_all(dp, c, std::make_index_sequence<kNumOrient>{});
+  __syncthreads();
+  const int nb = B - b0 < bpw ? B - b0 : bpw;
+  int cnt[MaxBoards];
+#pragma unroll
+  for (int jj = 0; jj < MaxBoards; ++jj) cnt[jj] = 0;
+  auto pack_one = [&](int p, const uint4 e) {
+    const uint64_t e0 = (uint64_t)e.x | ((uint64_t)e.y << 32);
+    const uint64_t e1 = (uint64_t)e.z | ((uint64_t)e.w << 32);
+#pragma unroll
+    for (int jj = 0; jj < MaxBoards; ++jj) {
+      if (jj < nb) {
+        const uint32_t* sb = st32 + jj * kStageWords;
+        const uint32_t lo = pack_word(e0, sb);
+        const uint32_t hi = pack_word(e1, sb);
+        masks[(size_t)(b0 + jj) * dp.W64 + p] = (uint64_t)lo | ((uint64_t)hi << 32);
+        cnt[jj] += __popc(lo) + __popc(hi);
+      }
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < kPackPrefetch; ++i)
+    if (l + i * kWave < dp.W64) pack_one(l + i * kWave, pe[i]);
+  for (int p = l + kPackPrefetch * kWave; p < dp.W64; p += kWave) pack_one(p, pack[p]);
+#pragma unroll
+  for (int jj = 0; jj < MaxBoards; ++jj) {
+    if (jj < nb) {
+      const int s = wave_sum(cnt[jj]);
+      if (counts && l == 0) counts[b0 + jj] = s;
+    }
+  }
+}
+
 }  // namespace bk
