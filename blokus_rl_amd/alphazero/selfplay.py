@@ -126,10 +126,11 @@ class SelfPlay:
                  cpuct: float = 1.0, temperature: float = 1.0, dirichlet_alpha: float = 1.0,
                  dirichlet_weight: float = 0.25, node_cap: int | None = None, child_cap: int | None = None,
                  cap: int = 2048, seed: int = 0, nn_dtype: torch.dtype = torch.float32, use_graph: bool = True,
-                 continuous: bool = False):
+                 continuous: bool = False, sim_graph_sims: int | None = None):
         self.eng = eng
         self.G = games
         self.num_sims = num_sims
+        self.sim_graph_sims = sim_graph_sims or self.SIM_GRAPH_SIMS or self.graph_sims_for(num_sims)
         self.cpuct = cpuct
         self.temperature = temperature
         self.alpha = dirichlet_alpha
@@ -228,8 +229,18 @@ class SelfPlay:
         logp, v, mode = self._evaluate(obs)
         self.mcts.expand_backup(logp, v, prior_mode=mode)
 
-    # simulations per captured graph (BK_SIM_GRAPH_SIMS; a ply's n simulations = n // k replays + eager rest)
-    SIM_GRAPH_SIMS = int(os.environ.get("BK_SIM_GRAPH_SIMS", "10"))
+    # simulations per captured graph (BK_SIM_GRAPH_SIMS or the constructor's sim_graph_sims; a ply's
+    # n simulations = n // k replays + eager rest). Default: the whole ply in one graph (one k_select
+    # per ply instead of one per replay: +0.5% sims/s at 100 sims vs k = 10), see graph_sims_for
+    SIM_GRAPH_SIMS = int(os.environ.get("BK_SIM_GRAPH_SIMS", "0"))
+
+    @staticmethod
+    def graph_sims_for(num_sims: int) -> int:
+        """num_sims itself up to 100, else its largest divisor <= 100 (10 if that is below 10)."""
+        if num_sims <= 100:
+            return max(num_sims, 1)
+        d = max(k for k in range(1, 101) if num_sims % k == 0)
+        return d if d >= 10 else 10
 
     def fused(self) -> bool:
         """Whole simulations in one launch (k_sims: the HIP ResNet in fp32 with the sparse policy
@@ -244,7 +255,7 @@ class SelfPlay:
 
     def _simulations(self, n: int):
         """n simulations of every active tree: fused launches (fused()), else replays of a graph of
-        SIM_GRAPH_SIMS captured simulations (no per-launch host work) and eager ones."""
+        sim_graph_sims captured simulations (no per-launch host work) and eager ones."""
         if self.fused():
             ev = self.evaluator
             k = self.sims_per_launch if self.sims_per_launch > 0 else max(n, 1)
@@ -255,7 +266,7 @@ class SelfPlay:
                 else:
                     self.mcts.simulate_resnet(self.roots, self.active, self.cpuct, c, ev.model)
             return
-        k = self.SIM_GRAPH_SIMS
+        k = self.sim_graph_sims
         if n >= k and self._graph_usable():
             g = self._sim_graph()
             self._g_roots.copy_(self.roots)
@@ -286,9 +297,9 @@ class SelfPlay:
             self.mcts.expand_backup(out, v, prior_mode=0)
 
     def _sim_graph(self):
-        """SIM_GRAPH_SIMS simulations captured once. With the sparse policy head the search half of
+        """sim_graph_sims simulations captured once. With the sparse policy head the search half of
         a simulation and the next one's descent are one launch (bk_mcts_leaf_step): select, then
-        SIM_GRAPH_SIMS x {net, leaf_step (+ select, except the last)} — the trees of the per-stage
+        sim_graph_sims x {net, leaf_step (+ select, except the last)} — the trees of the per-stage
         launches, bitwise (tests/test_sims_gpu.py)."""
         if self._graph is None:
             self._g_roots = self.roots.clone()
@@ -298,13 +309,13 @@ class SelfPlay:
             with torch.cuda.graph(g):
                 if ev.model is not None and ev.sparse:
                     _, obs, _ = self.mcts.select(self._g_roots, self._g_active, self.cpuct)
-                    for i in range(self.SIM_GRAPH_SIMS):
+                    for i in range(self.sim_graph_sims):
                         out, v = ev._forward(obs)
-                        last = i == self.SIM_GRAPH_SIMS - 1
+                        last = i == self.sim_graph_sims - 1
                         self.mcts.leaf_step(out, ev.policy_w, ev.policy_b, v, None if last else self._g_roots,
                                             self._g_active, self.cpuct)
                 else:
-                    for _ in range(self.SIM_GRAPH_SIMS):
+                    for _ in range(self.sim_graph_sims):
                         self._sim_body()
             self._graph = g
         return self._graph

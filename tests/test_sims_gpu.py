@@ -1,7 +1,7 @@
 """Whole simulations in one launch (bk_mcts_simulate_resnet / _const, sims.hip) against the
 per-stage launches they fuse (select -> leaf ResNet -> sparse policy head -> expand/backup, one
 launch each over all trees): the trees, counters and self-play plies come out bitwise identical.
-Also the captured simulation graph (SelfPlay.SIM_GRAPH_SIMS) against eager launches."""
+Also the captured simulation graph (SelfPlay.sim_graph_sims) against eager launches."""
 import pytest
 import torch
 
@@ -92,10 +92,11 @@ def test_leaf_step_matches_stagewise(N, T, sims):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("fused,graph", [("1", "1"), ("0", "1")])
-def test_selfplay_plies_match_eager(monkeypatch, fused, graph):
-    """The default play_ply paths (fused simulations, or the captured simulation graph) give the
-    plies of launching every stage eagerly."""
+@pytest.mark.parametrize("fused,graph,gsims", [("1", "1", None), ("0", "1", None), ("0", "1", 10)])
+def test_selfplay_plies_match_eager(monkeypatch, fused, graph, gsims):
+    """The default play_ply paths (fused simulations, or the captured simulation graph: the whole
+    ply in one graph, or 10 per graph + eager rest) give the plies of launching every stage
+    eagerly."""
     from blokus_rl_amd.alphazero.selfplay import SelfPlay
     from blokus_rl_amd.engine import Engine
     from blokus_rl_amd.nets import ResNet
@@ -109,7 +110,8 @@ def test_selfplay_plies_match_eager(monkeypatch, fused, graph):
         monkeypatch.setenv("BK_SIM_GRAPH", g)
         torch.manual_seed(0)
         model = ResNet(20, 4, eng.A, num_res_blocks=2).to(eng.device).eval()
-        sp = SelfPlay(eng, model, 6, num_sims=13, node_cap=256, seed=5, continuous=True)
+        sp = SelfPlay(eng, model, 6, num_sims=13, node_cap=256, seed=5, continuous=True,
+                      sim_graph_sims=gsims if g == "1" else None)
         for _ in range(3):
             sp.play_ply()
         _, n, q, p, k = sp.mcts.root_stats(sp.roots)
