@@ -32,15 +32,55 @@ HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
 LEGAL_BYTES_PER_BOARD = 384 + 3808 + 4
 
 
-def _dist_init():
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` started as one process: start N rank processes of this same script
+    (torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1) as CHILD processes and
+    return their exit code. Called before anything touches the GPU (this process never
+    initialises HIP). Rank 0 prints the one JSON line; the children inherit stdout."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env, check=False).returncode
+
+
+def dist_backend() -> str:
+    """RCCL ("nccl") on GPUs; gloo on CPU or when BK_DIST_BACKEND=gloo (several ranks sharing
+    one GPU in a rehearsal: RCCL refuses two ranks on one device)."""
+    b = os.environ.get("BK_DIST_BACKEND")
+    if b:
+        return b
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def _dist_init(need_gpu: bool = True):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if need_gpu:
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise RuntimeError("bench.py: no HIP device visible (the workloads run on the GPU; "
+                               "--workload dry rehearses the launch on CPU)")
+        dev = local % ndev  # one rank per GPU; a gloo rehearsal may put several ranks on one
+        torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        backend = dist_backend() if need_gpu else "gloo"
+        kw = {"device_id": torch.device("cuda", torch.cuda.current_device())} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
     return world, rank, local
 
 
@@ -49,10 +89,14 @@ def _barrier(world):
         dist.barrier()
 
 
+def _coll_device():
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+
 def _max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -60,9 +104,40 @@ def _max_over_ranks(x: float, world: int) -> float:
 def _sum_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t)
     return float(t.item())
+
+
+def bench_dry(args, world, rank):
+    """--workload dry: the multi-rank launch rehearsed on CPU (gloo, no GPU touched): every rank
+    packs a shard of synthetic replay rows (seeded by rank, ragged counts) and the ranks run the
+    config-4 exchange, all_gather_packed; rank 0 reports which ranks' rows arrived intact."""
+    from blokus_rl_amd import replay as rp
+
+    g = torch.Generator().manual_seed(rank)
+    E, K = 3 + rank, 40 + 10 * rank
+    states = torch.full((E, rp.STATE), rank, dtype=torch.uint8)
+    k = torch.full((E,), K, dtype=torch.int32)
+    ids = torch.randint(0, 30433, (E, K), generator=g).to(torch.int16)
+    pi = torch.rand((E, K), generator=g)
+    z = torch.zeros((E, 4))
+    buf, cap = rp.pack(states, ids, pi, k, z)
+    _barrier(world)
+    t0 = time.perf_counter()
+    if world > 1:
+        rows, cap = rp.all_gather_packed(buf, cap)
+    else:
+        rows = buf
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    u = rp.unpack(rows, cap)
+    seen = sorted({int(s) for s in u["states"][:, 0].tolist()})
+    return {"metric": "launch rehearsal (gloo, CPU): replay rows all-gathered", "value": float(rows.shape[0]),
+            "unit": "rows", "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": dt * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "dry", "parallelism": f"dp{world}"}, "ranks_seen": seen,
+            "backend": dist.get_backend() if world > 1 else None}
 
 
 def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
@@ -380,7 +455,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train", "ppo"], default="all")
+    ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train", "ppo", "dry"],
+                    default="all")
     ap.add_argument("--ppo-updates", type=int, default=2)
     ap.add_argument("--train-batch", type=int, default=1024)
     ap.add_argument("--train-steps", type=int, default=20)
@@ -401,7 +477,21 @@ def main():
     ap.add_argument("--node-cap", type=int, default=None,
                     help="nodes per tree (default: sims x the longest game + 1, SelfPlay.node_cap_for)")
     args = ap.parse_args()
-    world, rank, _ = _dist_init()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process started with --gpus N: become the launcher of N ranks (nothing here has
+        # touched the GPU; the ranks are child processes, not an exec of this one)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, _ = _dist_init(need_gpu=args.workload != "dry")
+    if args.workload == "dry":
+        out = bench_dry(args, world, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that run",
+              file=sys.stderr)
     if args.workload == "legal":
         out = bench_legal(args, world, rank)
     elif args.workload == "vecenv":

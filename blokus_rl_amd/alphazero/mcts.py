@@ -15,12 +15,34 @@ import torch
 from .batched_mcts import BatchedMCTS
 
 
+# simulations per move assumed when the game carries no hparams.num_mcts_sims: the reference docs'
+# arena setting (docs/README.md:159)
+DEFAULT_SIMS = 200
+
+
+def node_cap_for(game, sims: int | None = None) -> int:
+    """Nodes one tree needs for a whole game: the reference tree grows without bound (mcts.py:67-70),
+    a simulation adds at most one node and a game lasts at most pieces x players plies, so
+    sims x max plies + 1 (sims from the game's hparams.num_mcts_sims / arena_num_mcts_sims, the
+    largest of the two and DEFAULT_SIMS); a fuller tree raises EngineError at the expansion that
+    does not fit (MCTS.simulate checks every expansion)."""
+    eng = game.engine
+    if sims is None:
+        h = getattr(game, "hparams", None)
+        cand = [int(getattr(h, k)) for k in ("num_mcts_sims", "arena_num_mcts_sims")
+                if h is not None and isinstance(getattr(h, k, None), (int, float))]
+        sims = max(cand + [DEFAULT_SIMS])
+    return int(sims) * eng.num_pieces * eng.P + 1
+
+
 class MCTS:
-    def __init__(self, game, nn, node_cap: int = 16384, child_cap: int | None = None):
+    def __init__(self, game, nn, node_cap: int | None = None, child_cap: int | None = None):
         self.game = game
         self.nn = nn
         eng = game.engine
         self._eng = eng
+        if node_cap is None:
+            node_cap = node_cap_for(game)
         self._m = BatchedMCTS(eng, 1, node_cap=node_cap, child_cap=child_cap or node_cap * (256 if eng.N >= 14 else 64))
         self._logp = torch.zeros((1, eng.A), dtype=torch.float32, device=eng.device)
         self._vals = torch.zeros((1, eng.P), dtype=torch.float32, device=eng.device)
@@ -40,6 +62,7 @@ class MCTS:
             leaves, _ = self._m.leaf_info()
             _, scores = self._eng.game_ended(leaves)
             self._m.expand_backup(self._logp, self._vals, prior_mode=1)
+            self._m.check()
             return scores[0].cpu().numpy()
         if st != 1:
             self._m.check()
@@ -47,6 +70,7 @@ class MCTS:
         if hasattr(self.nn, "predict_batch"):
             logp, v = self.nn.predict_batch(obs)
             self._m.expand_backup(logp, v, prior_mode=0)
+            self._m.check()  # a full node/child table raises here instead of distorting pi
             return v[0].cpu().numpy()
         mask_f = self._eng.unpack_mask(mask)[0].cpu().numpy().astype(np.float64)
         p, v = self.nn.predict(obs[0].cpu().numpy(), mask_f)
@@ -55,6 +79,7 @@ class MCTS:
         self._logp[0, ids] = torch.as_tensor(np.atleast_1d(p), dtype=torch.float32, device=self._eng.device)
         self._vals[0] = torch.as_tensor(np.asarray(v, dtype=np.float32), device=self._eng.device)
         self._m.expand_backup(self._logp, self._vals, prior_mode=1)
+        self._m.check()
         return v
 
     def get_distribution(self, s, temperature):

@@ -126,17 +126,24 @@ class SelfPlay:
                  cpuct: float = 1.0, temperature: float = 1.0, dirichlet_alpha: float = 1.0,
                  dirichlet_weight: float = 0.25, node_cap: int | None = None, child_cap: int | None = None,
                  cap: int = 2048, seed: int = 0, nn_dtype: torch.dtype = torch.float32, use_graph: bool = True,
-                 continuous: bool = False, sim_graph_sims: int | None = None):
+                 continuous: bool = False, sim_graph_sims: int | None = None, record_plies: int | None = None):
         self.eng = eng
         self.G = games
         self.num_sims = num_sims
-        self.sim_graph_sims = sim_graph_sims or self.SIM_GRAPH_SIMS or self.graph_sims_for(num_sims)
+        # BK_SIM_GRAPH_SIMS is read here (not at import) like the other BK_* knobs
+        self.sim_graph_sims = (sim_graph_sims or int(os.environ.get("BK_SIM_GRAPH_SIMS", "0"))
+                               or self.graph_sims_for(num_sims))
         self.cpuct = cpuct
         self.temperature = temperature
         self.alpha = dirichlet_alpha
         self.weight = dirichlet_weight
         self.cap = cap
         self.continuous = continuous
+        # records kept on the device (~3 MB per ply at 256 games): all of them in finite mode (a run
+        # ends with every game), the last `record_plies` plies in continuous mode, where games never
+        # stop (examples(drain=True) / window_packed() take them out; older plies are dropped)
+        self.record_plies = record_plies if record_plies is not None else (
+            4 * self.max_game_plies(eng) if continuous else 0)
         if node_cap is None:
             node_cap = self.node_cap_for(eng, num_sims)
         self.mcts = BatchedMCTS(eng, games, node_cap=node_cap, child_cap=child_cap)
@@ -167,6 +174,7 @@ class SelfPlay:
         # fused path: simulations per launch (0: all of a ply's in one launch)
         self.sims_per_launch = int(os.environ.get("BK_SIMS_PER_LAUNCH", "0"))
         self._window: list[tuple[torch.Tensor, ...]] = []  # records since mark_window()
+        self._dropped_plies = 0  # continuous mode: plies that fell out of the record ring
         # an active game whose root had more children than `cap` (k_root returns counts = -K):
         # latched on the device, raised by check() at the next host sync
         self._cap_overflow = torch.zeros((), dtype=torch.int32, device=dev)
@@ -229,10 +237,9 @@ class SelfPlay:
         logp, v, mode = self._evaluate(obs)
         self.mcts.expand_backup(logp, v, prior_mode=mode)
 
-    # simulations per captured graph (BK_SIM_GRAPH_SIMS or the constructor's sim_graph_sims; a ply's
+    # simulations per captured graph (the constructor's sim_graph_sims or BK_SIM_GRAPH_SIMS; a ply's
     # n simulations = n // k replays + eager rest). Default: the whole ply in one graph (one k_select
     # per ply instead of one per replay: +0.5% sims/s at 100 sims vs k = 10), see graph_sims_for
-    SIM_GRAPH_SIMS = int(os.environ.get("BK_SIM_GRAPH_SIMS", "0"))
 
     @staticmethod
     def graph_sims_for(num_sims: int) -> int:
@@ -371,6 +378,10 @@ class SelfPlay:
                    act_mask.clone())
             self._records.append(rec)
             self._window.append(rec)
+            if self.record_plies and len(self._records) > self.record_plies:
+                self._dropped_plies += len(self._records) - self.record_plies
+                del self._records[:-self.record_plies]
+                del self._window[:-self.record_plies]
         self.roots, _, status = self.eng.next_state(self.roots, action)
         self.first_ply &= ~act_mask
         self._stats.plies += 1

@@ -246,6 +246,23 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
   const size_t T = (size_t)trees;
   const int W64 = ctx->dp.W64;
   int rc = hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+  if (!rc) {
+    // the whole allocation checked against the device's free memory first: an oversized tree set
+    // (node_cap grows with the simulations per move) fails here with its size, not inside hipMalloc
+    const size_t C0 = (size_t)d.child_cap_per_tree * T;
+    const size_t need = T * TS * sizeof(TabEntry) + C0 * (4 + 4 + 8 + 4) +
+                        T * (kMaxDepth * 12 + kStateWords * 4 + kMaxP * 8 + W64 * 8 + kLeafCap * 8 + 64 + 64);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && need > free_b) {
+      delete m;
+      char msg[256];
+      snprintf(msg, sizeof msg,
+               "bk_mcts_create: %d trees x node_cap %d (child_cap %lld) need %.2f GB of device memory, %.2f GB free",
+               trees, node_cap, (long long)child_cap, need / 1e9, free_b / 1e9);
+      bk::set_error(msg);
+      return BK_ENOMEM;
+    }
+  }
   if (!rc) rc = mcts_alloc(m, &d.tab, T * TS);
   if (!rc) rc = mcts_alloc(m, &d.tree_nodes, T);
   if (!rc) rc = mcts_alloc(m, &d.tree_children, T);

@@ -253,6 +253,9 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     scanned += Kn;
     int a, ci;
     BK_TACC(t_child, ci = select_child(m, off, Kn, cp, a));
+    // no child won the argmax: every PUCT score was NaN (a NaN prior or value from a diverged
+    // net); flag it and stop before the unchecked placement and the path record
+    if (ci < 0 || ci >= Kn) { err |= kErrIllegal; break; }
     if (depth >= kMaxDepth) { err |= kErrDepth; break; }
     // the child's action is legal by construction (its id came from the node's legal mask)
     const int p = (int)s[kWToMove];

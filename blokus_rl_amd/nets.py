@@ -472,10 +472,19 @@ class LeafResNet(nn.Module):
                 self.register_buffer("x3_wtower", torch.cat([p[0] for p in packs]).contiguous())
                 self.register_buffer("x3_stower", torch.cat([p[1] for p in packs]).contiguous())
                 self.register_buffer("x3_bounds", torch.cat([bs] + [p[2] for p in packs]).contiguous())
-                c = lambda t: t.detach().float().contiguous()  # noqa: E731
-                self.x3_heads = [c(f.stem.bias), c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias),
-                                 c(f.value_conv.weight.view(64)), c(f.value_conv.bias), f.value_fc1_wt(),
-                                 c(f.value_fc1.bias), c(f.value_fc2.weight), c(f.value_fc2.bias)]
+                c = lambda t: t.detach().float().contiguous().clone()  # noqa: E731
+                heads = [c(f.stem.bias), c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias),
+                         c(f.value_conv.weight.view(64)), c(f.value_conv.bias), c(f.value_fc1_wt()),
+                         c(f.value_fc1.bias), c(f.value_fc2.weight), c(f.value_fc2.bias)]
+                # registered buffers, so .to(device) / state_dict see them like the weight packs
+                for i, t in enumerate(heads):
+                    self.register_buffer(f"x3_head{i}", t)
+
+    @property
+    def x3_heads(self) -> list[torch.Tensor]:
+        """bk_leafnet_x3's head operands (stem bias, policy/value 1x1 convs, value MLP), on the
+        module's current device."""
+        return [getattr(self, f"x3_head{i}") for i in range(9)]
 
     @torch.no_grad()
     def forward(self, x):

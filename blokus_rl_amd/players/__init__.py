@@ -20,11 +20,12 @@ class MCTSPlayer(Player):
     """players/mcts_player.py:8-28: `simulations` searches, then the T=0 (argmax) move."""
 
     def __init__(self, game, nn, simulations):
-        from ..alphazero.mcts import MCTS
+        from ..alphazero.mcts import MCTS, node_cap_for
 
         self.game, self.nn, self.simulations = game, nn, simulations
         self._mcts_cls = MCTS
-        self.tree = MCTS(game, nn)
+        self._node_cap = max(node_cap_for(game), node_cap_for(game, simulations))
+        self.tree = MCTS(game, nn, node_cap=self._node_cap)
 
     def update_state(self, s, current_player):
         for _ in range(self.simulations):
@@ -34,7 +35,7 @@ class MCTSPlayer(Player):
         return self.game.get_next_state(s, current_player, a[0])
 
     def reset(self):
-        self.tree = self._mcts_cls(self.game, self.nn)
+        self.tree = self._mcts_cls(self.game, self.nn, node_cap=self._node_cap)
 
     def __str__(self):
         return "MCTSPlayer"

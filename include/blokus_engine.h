@@ -32,7 +32,7 @@ extern "C" {
 #define BK_EHIP -2      /* a HIP runtime call failed                             */
 #define BK_EILLEGAL -3  /* an action is not legal in its state (next_state)     */
 #define BK_ECAPACITY -4 /* an MCTS pool/table ran out of room                    */
-#define BK_ENOMEM -5
+#define BK_ENOMEM -5    /* the requested device allocation exceeds free memory  */
 
 /* ---------------------------------------------------------------- packed state
  * One game state = 384 bytes (6 x 64 B), 64-B aligned in arrays. Byte layout:

@@ -67,3 +67,22 @@ def test_all_gather_packed_world2_gloo():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_bench_launches_ranks_itself():
+    """`python bench.py --gpus 2` started as ONE process (as the driver starts it) launches two
+    ranks itself (torch.distributed.run, 127.0.0.1) and rank 0 prints one JSON line. The dry
+    workload rehearses it on CPU over gloo: both ranks' replay rows reach rank 0."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "dry"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == [0, 1] and out["value"] == 3 + 4

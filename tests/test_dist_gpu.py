@@ -1,0 +1,33 @@
+"""The config-4 path with several ranks on the one GPU of a test box: `bench.py --gpus 2` launches
+two ranks itself; with BK_DIST_BACKEND=gloo both ranks share cuda:0 (RCCL refuses two ranks on
+one device), so this rehearses everything of the 8-GPU run except RCCL itself — the launcher,
+per-rank game seeds, the timed plies, the all-gather of the (s, pi, z) rows and the max-over-
+ranks timing."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_selfplay_two_ranks_one_gpu():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BK_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "selfplay", "--games", "16",
+           "--sims", "4", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    # 2 ranks x 16 games x 4 sims x 3 plies
+    assert out["engine_counters"]["expanded"] + out["engine_counters"]["terminal"] >= 16 * 4 * 3 - 16 * 3
+    assert abs(out["value"] * out["ms_per_step"] * 1e-3 * out["steps"] - 2 * 16 * 4 * 3) < 1e-6 * 2 * 16 * 4 * 3 + 1
+    ag = out["stage_ms_per_sim_step"]["all_gather"]
+    assert ag["rows_sent"] == 16 * 3 and ag["rows_received"] == 2 * ag["rows_sent"]

@@ -101,3 +101,17 @@ def test_leaf_resnet_default_math_is_x3(monkeypatch):
     pf32, v32 = leaf(obs)
     assert not torch.equal(pf32, pf)
     assert torch.allclose(pf32, pf, rtol=1e-5, atol=1e-5) and torch.allclose(v32, v, rtol=1e-5, atol=1e-6)
+
+
+def test_leaf_resnet_head_operands_are_buffers():
+    """The x3 head operands are registered buffers: state_dict carries them and .to() moves them
+    with the weight packs (a plain list kept device pointers of the old location)."""
+    from blokus_rl_amd.nets import LeafResNet
+
+    leaf = LeafResNet(_net(20, 1, seed=5), normalize=False, features=True).eval()
+    sd = leaf.state_dict()
+    assert all(f"x3_head{i}" in sd for i in range(9))
+    cpu = leaf.to("cpu")
+    assert all(t.device.type == "cpu" for t in cpu.x3_heads) and cpu.x3_wtower.device.type == "cpu"
+    back = cpu.to("cuda")
+    assert all(t.is_cuda for t in back.x3_heads)

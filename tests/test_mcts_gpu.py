@@ -136,3 +136,27 @@ def test_masked_softmax_prior_matches_torch(engines):
         ref = torch.exp(torch.log_softmax(torch.masked_select(logp[t], bits[t]), dim=-1))
         assert torch.equal(ids[t, :K].long(), torch.nonzero(bits[t]).view(-1))
         torch.testing.assert_close(p[t, :K], ref, rtol=2e-6, atol=1e-7)
+
+
+def test_nan_priors_flag_an_error_instead_of_faulting(engines):
+    """A diverged net (NaN priors and values): no child wins the PUCT argmax, so the descent
+    flags kErrIllegal and stops (status 0) — no placement, no out-of-range path record — and
+    check() raises; the next expand_backup is a no-op for that tree."""
+    from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
+    from blokus_rl_amd.engine import EngineError
+
+    eng = engines[(20, 4, 5)]
+    T = 2
+    m = BatchedMCTS(eng, T, node_cap=64, child_cap=T * 64 * 1024)
+    roots = eng.init_states(T)
+    logp = torch.full((T, eng.A), float("nan"), dtype=torch.float32, device=eng.device)
+    vals = torch.full((T, eng.P), float("nan"), dtype=torch.float32, device=eng.device)
+    status, _, _ = m.select(roots, None, 1.0)
+    assert status.tolist() == [1, 1]
+    m.expand_backup(logp, vals, prior_mode=0)  # the roots expand with NaN priors
+    status, _, _ = m.select(roots, None, 1.0)
+    assert status.tolist() == [0, 0]
+    m.expand_backup(logp, vals, prior_mode=0)
+    torch.cuda.synchronize()
+    with pytest.raises(EngineError):
+        m.check()
