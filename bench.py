@@ -157,6 +157,130 @@ def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
     return None
 
 
+# ----------------------------------------------------------------------------- CPU baselines
+# The reference-equivalent CPU paths (oracle/: the C restatement of the rules and the Python
+# restatement of mcts.py) on every host core the box gives this job: one worker process per core
+# ("one game per process on all host cores"), started before the benchmark touches
+# the GPU (spawned, idle until the GPU legs are done), each running its own bounded sample.
+
+def cpu_workers() -> int:
+    """Host cores for the CPU baselines: BK_CPU_WORKERS, else the cores this process may run on,
+    capped at 16 (a GPU box's CPU share for one GPU; nproc there shows the whole machine)."""
+    n = os.environ.get("BK_CPU_WORKERS")
+    if n:
+        return max(1, int(n))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail))
+
+
+def start_cpu_pool(n: int):
+    import multiprocessing as mp
+
+    return mp.get_context("spawn").Pool(n)
+
+
+def _pool_run(pool, fn, jobs):
+    """Run jobs (one per worker) concurrently -> (sum of units, max seconds, per-worker units)."""
+    res = pool.map(fn, jobs) if pool is not None else [fn(j) for j in jobs]
+    return sum(r[0] for r in res), max(r[1] for r in res), [r[0] for r in res]
+
+
+def _w_legal(job):
+    """Worker: legal masks of its share of the benchmark boards (C oracle), repeated for `seconds`."""
+    states, seconds = job
+    from oracle.oracle import Oracle
+
+    o = Oracle(20, 4, 5)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.legal_mask_batch(states)
+        n += states.shape[0]
+    return n, time.perf_counter() - t0
+
+
+def _w_vecenv(job):
+    seconds, seed = job
+    from oracle.vecenv_oracle import VecEnvOracle
+
+    ref = VecEnvOracle(64, 7, 4)
+    ref.reset(seed)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for e in range(64):
+            ref.step(e, -1)
+        n += 64
+    return n, time.perf_counter() - t0
+
+
+def _w_config1(job):
+    """Worker: 7x7 games from default_rng(seed) (uniform legal moves) to terminal on the C oracle,
+    counting get_valid_moves + step calls."""
+    cells, seed0, seconds = job
+    from oracle.oracle import Oracle
+
+    o = Oracle(7, 2, cells)
+    calls, seed, t0 = 0, seed0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        rng = np.random.default_rng(seed)
+        st = o.init_state()
+        while o.game_ended(st) is None:
+            ids = o.legal_ids(st)
+            st, _ = o.next_state(st, int(ids[int(rng.integers(len(ids)))]))
+            calls += 2
+        seed += 1
+    return calls, time.perf_counter() - t0
+
+
+def _w_selfplay(job):
+    """Worker: the reference-equivalent self-play of cpu_baseline_selfplay for `seconds`, its own
+    game (moves sampled from pi at T=1 with default_rng(seed))."""
+    seconds, model_type, seed = job
+    return _selfplay_sample(seconds, model_type, seed)
+
+
+def _selfplay_sample(seconds: float, model_type: str, seed: int):
+    from blokus_rl_amd.nets import build_model
+    from oracle.oracle import MCTSOracle, Oracle
+
+    o = Oracle(20, 4, 5)
+    torch.manual_seed(0)
+    model = None
+    if model_type != "dumbnet":
+        torch.cuda.set_device(0)
+        model = build_model(model_type, 20, 4, o.A, num_res_blocks=5).cuda().eval()
+
+    def evaluate(s, player):
+        ids = o.legal_ids(s, player)
+        if model is None:
+            return ids, np.full(len(ids), 1.0 / len(ids), dtype=np.float32), np.zeros(4)
+        obs = torch.from_numpy(o.observe(s)).float().cuda().unsqueeze(0)
+        mask = torch.zeros(o.A, dtype=torch.bool, device="cuda")
+        mask[torch.from_numpy(ids).cuda()] = True
+        with torch.inference_mode():
+            lp, v = model(obs)
+            p = torch.exp(torch.log_softmax(torch.masked_select(lp[0], mask), dim=-1))
+        return ids, p.cpu().numpy(), v[0].cpu().numpy().astype(np.float64)
+
+    rng = np.random.default_rng(seed)
+    m = MCTSOracle(o, evaluate)
+    s = o.init_state()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(100):
+            m.simulate(s)
+            n += 1
+        ids, pi = m.get_distribution(s, 1)
+        pi = np.asarray(pi, dtype=np.float64)
+        s, _ = o.next_state(s, int(ids[int(rng.choice(len(ids), p=pi / pi.sum()))]))
+        if o.game_ended(s) is not None:
+            m = MCTSOracle(o, evaluate)
+            s = o.init_state()
+    return n, time.perf_counter() - t0
+
+
 # ----------------------------------------------------------------------------- legal
 def bench_legal(args, world, rank):
     from blokus_rl_amd.boards import random_boards
@@ -241,26 +365,20 @@ def bench_legal(args, world, rank):
                      "bytes_per_unit": LEGAL_BYTES_PER_BOARD, "units_per_launch": B},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_legal(states, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline_legal(states, args.cpu_seconds, args.cpu_pool, args.cpu_workers)
     out["_states"] = states
     return out
 
 
-def cpu_baseline_legal(states: torch.Tensor, seconds: float):
-    """The oracle (C restatement of the reference rules, 1 core) on a bounded sample of the
-    same boards: repeat over the first 256 boards until `seconds` of CPU work."""
-    from oracle.oracle import Oracle
-
-    o = Oracle(20, 4, 5)
-    sample = states[:256].cpu().numpy()
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.legal_mask_batch(sample)
-        n += sample.shape[0]
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "boards/s", "cores": 1, "kind": "port",
-            "sample": f"{n} board evaluations (first 256 benchmark boards, repeated) in {dt:.1f} s"}
+def cpu_baseline_legal(states: torch.Tensor, seconds: float, pool=None, workers: int = 1):
+    """The oracle (C restatement of the reference rules) on a bounded sample of the same boards:
+    each worker repeats its share of the first 64 x workers boards until `seconds` pass."""
+    sample = states[: 64 * workers].cpu().numpy()
+    shares = [np.ascontiguousarray(x) for x in np.array_split(sample, workers)]
+    n, dt, _ = _pool_run(pool, _w_legal, [(sh, seconds) for sh in shares])
+    return {"value": n / dt, "unit": "boards/s", "cores": workers, "kind": "port",
+            "sample": f"{n} board evaluations ({sample.shape[0]} benchmark boards split over {workers} worker "
+                      f"processes, repeated) in {dt:.1f} s"}
 
 
 # Config 5 algorithmic bytes per env-step: state read + write (768), action (4), rng (16),
@@ -312,69 +430,89 @@ def bench_vecenv(args, world, rank):
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
                         "kernel_ms": kernel_ms, "bytes_per_unit": VEC_BYTES_PER_STEP, "units_per_launch": E}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2)
+        out["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2, args.cpu_pool, args.cpu_workers)
     return out
 
 
-def cpu_baseline_vecenv(seconds: float):
+def cpu_baseline_vecenv(seconds: float, pool=None, workers: int = 1):
     """The config-5 env restated on the CPU (oracle/vecenv_oracle.py: C oracle rules, Python
-    loop per env like SyncVectorEnv), random agent + random opponent, 1 core."""
-    from oracle.vecenv_oracle import VecEnvOracle
-
-    ref = VecEnvOracle(64, 7, 4)
-    ref.reset(0)
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        for e in range(64):
-            ref.step(e, -1)
-        n += 64
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} env steps of 64 sequential 7x7 envs in {dt:.1f} s"}
+    loop per env like SyncVectorEnv), random agent + random opponent, 64 envs per worker."""
+    n, dt, _ = _pool_run(pool, _w_vecenv, [(seconds, w) for w in range(workers)])
+    return {"value": n / dt, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": f"{n} env steps of 64 sequential 7x7 envs per worker x {workers} workers in {dt:.1f} s"}
 
 
-def cpu_baseline_selfplay(seconds: float, model_type: str = "resnet"):
+def cpu_baseline_selfplay(seconds: float, model_type: str = "resnet", pool=None, workers: int = 1):
     """Reference-equivalent CPU path: the pure-Python restatement of
-    MCTS.simulate (oracle/oracle.py, float64, dict-keyed tree), the C oracle env on 1 host core,
-    and — for resnet — batch-1 leaf evaluation of the unfused ResNet on the GPU with a host
-    round trip per leaf exactly like BlokusNNetWrapper.predict (neural_network.py:92-110).
-    One game from the empty board, 100 simulations per move, argmax moves, until `seconds`."""
-    from blokus_rl_amd.nets import build_model
-    from oracle.oracle import MCTSOracle, Oracle
+    MCTS.simulate (oracle/oracle.py, float64, dict-keyed tree) and the C oracle env, one game per
+    worker process on `workers` host cores; for resnet, batch-1 leaf evaluation of the unfused
+    ResNet on the GPU with a host round trip per leaf exactly like BlokusNNetWrapper.predict
+    (neural_network.py:92-110). 100 simulations per move, moves sampled from pi (T=1)."""
+    n, dt, per = _pool_run(pool, _w_selfplay, [(seconds, model_type, w) for w in range(workers)])
+    return {"value": n / dt, "unit": "sims/s", "cores": workers, "kind": "port",
+            "per_core": float(np.mean(per)) / dt,
+            "sample": f"{n} simulations ({model_type} leaf eval{' on the GPU, batch 1' if model_type != 'dumbnet' else ''}"
+                      f"), one game per worker process x {workers} from the empty board, in {dt:.1f} s"}
 
-    o = Oracle(20, 4, 5)
-    torch.manual_seed(0)
-    model = build_model(model_type, 20, 4, o.A, num_res_blocks=5).cuda().eval() if model_type != "dumbnet" else None
 
-    def evaluate(s, player):
-        ids = o.legal_ids(s, player)
-        if model is None:
-            return ids, np.full(len(ids), 1.0 / len(ids), dtype=np.float32), np.zeros(4)
-        obs = torch.from_numpy(o.observe(s)).float().cuda().unsqueeze(0)
-        mask = torch.zeros(o.A, dtype=torch.bool, device="cuda")
-        mask[torch.from_numpy(ids).cuda()] = True
-        with torch.inference_mode():
-            lp, v = model(obs)
-            p = torch.exp(torch.log_softmax(torch.masked_select(lp[0], mask), dim=-1))
-        return ids, p.cpu().numpy(), v[0].cpu().numpy().astype(np.float64)
+def bench_config1(args, pool=None, workers: int = 1):
+    """Config 1: 7x7 2-player games, get_valid_moves + step to terminal, uniform random legal moves
+    from numpy default_rng(seed), for both 7x7 piece sets (2522 ids = all 21 pieces,
+    as the recordings show; 919 ids = pieces of <= 4 cells, the documented gym action space).
+    Engine legs: the drop-in ColosseumBlokusGameWrapper at batch 1 (each call a device round trip,
+    the reference's calling pattern) and the batched engine (1024 games in lock-step on the GPU,
+    device-side sampling). CPU leg: the C oracle, one worker process per host core."""
+    from types import SimpleNamespace
 
-    m = MCTSOracle(o, evaluate)
-    s = o.init_state()
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        for _ in range(100):
-            m.simulate(s)
-            n += 1
-        ids, pi = m.get_distribution(s, 0)
-        s, _ = o.next_state(s, int(ids[int(np.argmax(pi))]))
-        if o.game_ended(s) is not None:
-            s = o.init_state()
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "sims/s", "cores": 1, "kind": "port",
-            "sample": f"{n} simulations ({model_type} leaf eval{' on the GPU, batch 1' if model else ''}) "
-                      f"of one game from the empty board in {dt:.1f} s"}
+    from blokus_rl_amd.colossumrl import ColosseumBlokusGameWrapper
+
+    out = {"metric": "7x7 get_valid_moves + step calls/s (2 players, random legal moves to terminal)",
+           "unit": "calls/s"}
+    secs = max(1.0, args.cpu_seconds / 4)
+    for cells in (5, 4):
+        game = ColosseumBlokusGameWrapper(SimpleNamespace(board_size=7, number_of_players=2, max_piece_cells=cells))
+        calls, games, seed, t0 = 0, 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            rng = np.random.default_rng(seed)
+            s, p = game.get_init_board()
+            while game.get_game_ended(s) is None:
+                ids = np.nonzero(game.get_valid_moves(s, p))[0]
+                s, p = game.get_next_state(s, p, int(ids[int(rng.integers(len(ids)))]))
+                calls += 2
+            games += 1
+            seed += 1
+        dt_drop = time.perf_counter() - t0
+        eng = game.engine
+        G = 1024
+        gen = torch.Generator(device=eng.device).manual_seed(0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = eng.init_states(G)
+        plies = torch.zeros((), dtype=torch.int64, device=eng.device)
+        for i in range(4 * eng.num_pieces * eng.P):
+            ids, cnt = eng.legal_ids(st, cap=1024)
+            live = cnt > 0
+            pick = (torch.rand(G, device=eng.device, generator=gen) * cnt.clamp(min=1)).long()
+            act = torch.where(live, ids.gather(1, pick.view(-1, 1)).view(-1), torch.full_like(cnt, -1))
+            st, _, _ = eng.next_state(st, act.to(torch.int32).contiguous())
+            plies += live.sum()
+            if i % 8 == 7 and not bool(live.any()):
+                break
+        torch.cuda.synchronize()
+        dt_b = time.perf_counter() - t0
+        nb = 2 * int(plies)
+        rec = {"ids": eng.A,
+               "engine_dropin_batch1": {"value": calls / dt_drop, "unit": "calls/s", "games": games},
+               "engine_batched": {"value": nb / dt_b, "unit": "calls/s", "games": G,
+                                  "note": "legal-id enumeration + next state of 1024 games per launch pair"}}
+        if not args.no_cpu_baseline:
+            n, dt, _ = _pool_run(pool, _w_config1, [(cells, 100000 * w, secs) for w in range(workers)])
+            rec["cpu_baseline"] = {"value": n / dt, "unit": "calls/s", "cores": workers, "kind": "port",
+                                   "sample": f"{n} calls of 7x7 random games (C oracle, default_rng seeds), "
+                                             f"{workers} worker processes, {dt:.1f} s"}
+        out[f"ids_{eng.A}"] = rec
+    out["value"] = out["ids_2522"]["engine_batched"]["value"]
+    return out
 
 
 def bench_train(args, world, rank):
@@ -481,6 +619,12 @@ def main():
         # one process started with --gpus N: become the launcher of N ranks (nothing here has
         # touched the GPU; the ranks are child processes, not an exec of this one)
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    args.cpu_workers, args.cpu_pool = 1, None
+    if (not args.no_cpu_baseline and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.workload != "dry"
+            and args.workload not in ("train", "ppo")):
+        # the CPU-baseline worker processes, started before anything touches the GPU
+        args.cpu_workers = cpu_workers()
+        args.cpu_pool = start_cpu_pool(args.cpu_workers) if args.cpu_workers > 1 else None
     world, rank, _ = _dist_init(need_gpu=args.workload != "dry")
     if args.workload == "dry":
         out = bench_dry(args, world, rank)
@@ -507,6 +651,21 @@ def main():
         if kname.startswith("k_conv3x3") or kname.startswith("k_tower") or kname.startswith("k_leafnet"):
             # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)
             out["roofline"]["traffic"] = _pmc_traffic(kname, args.games)
+        if args.workload == "all" and args.model == "resnet" and args.nn_dtype == "fp32":
+            # the same self-play with the leaf net at the reference's own precision: every product
+            # on the exact-f32 MFMA (BK_NET_MATH=f32), timed the same way
+            from blokus_rl_amd.nets import net_math
+
+            if net_math() == "x3":
+                os.environ["BK_NET_MATH"] = "f32"
+                try:
+                    _, _, fsims, fdt, _, _ = run_selfplay("resnet", "fp32", args.games, args.sims, args.steps,
+                                                          args.warmup, rank, args.node_cap, world, timers=False)
+                finally:
+                    del os.environ["BK_NET_MATH"]
+                out["net_math_f32"] = {"value": _sum_over_ranks(fsims, world) / _max_over_ranks(fdt, world),
+                                       "unit": "sims/s", "dtype": "fp32 net: exact f32 MFMA products "
+                                       "(v_mfma_f32_16x16x4_f32, Winograd F(2x2,3x3) tower), BK_NET_MATH=f32"}
         if args.workload == "all":
             # env + search alone: the uninformed-MCTS opponent (DumbNet, compare_arena.py:87-95)
             _, _, dsims, dt, dctr, dms = run_selfplay("dumbnet", "fp32", args.games, args.sims, args.steps,
@@ -522,13 +681,19 @@ def main():
             vargs.no_cpu_baseline = True
             out["ppo_vector_env"] = bench_vecenv(vargs, world, rank)
             out["learner"] = bench_train(args, world, rank)
+            if world == 1:
+                out["config1_7x7"] = bench_config1(args, args.cpu_pool, args.cpu_workers)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_selfplay(args.cpu_seconds, args.model)
+            pool, nw = args.cpu_pool, args.cpu_workers
+            out["cpu_baseline"] = cpu_baseline_selfplay(args.cpu_seconds, args.model, pool, nw)
             if args.workload == "all":
-                out["cpu_baseline_uninformed"] = cpu_baseline_selfplay(args.cpu_seconds / 2, "dumbnet")
-                out["legal_move"]["cpu_baseline"] = cpu_baseline_legal(legal["_states"], args.cpu_seconds / 2)
-                out["ppo_vector_env"]["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2)
+                out["cpu_baseline_uninformed"] = cpu_baseline_selfplay(args.cpu_seconds / 2, "dumbnet", pool, nw)
+                out["legal_move"]["cpu_baseline"] = cpu_baseline_legal(legal["_states"], args.cpu_seconds / 2, pool, nw)
+                out["ppo_vector_env"]["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2, pool, nw)
     out.pop("_states", None)
+    if args.cpu_pool is not None:
+        args.cpu_pool.close()
+        args.cpu_pool.join()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -16,7 +16,6 @@ from ..engine import Engine
 from ..nets import build_model
 from .selfplay import SelfPlay
 
-RESNET_FLOPS_PER_LEAF = 347.5e6
 FP32_PEAK = 157.3e12             # MI355X_MICROARCH.md (f32 vector = f32 MFMA)
 FP16_PEAK = 2.5e15               # dense bf16/fp16 MFMA
 HBM_PEAK = 8.0e12
@@ -30,6 +29,59 @@ def search_bytes(c: dict, sims: int, obs_bytes: int, mask_bytes: int) -> float:
     of node/value; per created child 4 B logit gather + 20 B child init."""
     return (sims * 384 + c["scanned"] * 16 + c["levels"] * (52 + 40)
             + c["expanded"] * (384 + mask_bytes + obs_bytes + mask_bytes + 36) + c["leaf_children"] * 24)
+
+
+def leaf_step_bytes(c: dict, sims: int, N: int, P: int, W64: int, F: int) -> float:
+    """Algorithmic bytes of a sim-step's search launches on the timed path (k_select once per ply,
+    then k_leaf_step per simulation) from engine counters, as the kernels move them:
+    per simulation the root state (384); per descended level one 64-entry table probe (1 KB), the
+    node's child statistics (20 B each: P, N, Q, id), the path record (12) and its backup (24);
+    per expanded leaf the probe + entry (1040), the leaf state written and re-read (768), the legal
+    bitmask written and re-read (2 x 8 W64), the observation (4 x 2P N^2), the policy features
+    (4 F) and the value (16); per legal id of an expanded leaf its policy-Linear row and bias
+    (4 F + 4: the sparse head, rows shared between trees are counted per use) and the child
+    initialised (20)."""
+    return (sims * 384 + c["levels"] * (1024 + 12 + 24) + c["scanned"] * 20
+            + c["expanded"] * (1040 + 768 + 2 * 8 * W64 + 4 * 2 * P * N * N + 4 * F + 16)
+            + c["leaf_children"] * (4 * F + 4 + 20))
+
+
+def time_leaf_step(sp, n: int = 10):
+    """The search half of the timed path, live: one eager k_select, then n x {leaf net (graph
+    replay), k_leaf_step} with HIP events on the launch stream around each search launch (the
+    same kernels the captured ply graph replays). -> dict(ms per sim-step of the search
+    launches, bytes per sim-step, k_leaf_step us) or None (no sparse HIP net)."""
+    ev = sp.evaluator
+    if not ev.sparse or ev.graph is None:
+        return None
+    st = torch.cuda.current_stream(sp.eng.device)
+    E = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    torch.cuda.synchronize()
+    c0 = sp.mcts.counters()
+    e_sel = (E(), E())
+    e_sel[0].record(st)
+    _, obs, _ = sp.mcts.select(sp.roots, sp.active, sp.cpuct)
+    e_sel[1].record(st)
+    steps = []
+    for i in range(n):
+        out, v = ev(obs)
+        a, b = E(), E()
+        a.record(st)
+        last = i == n - 1
+        sp.mcts.leaf_step(out, ev.policy_w, ev.policy_b, v, None if last else sp.roots, sp.active, sp.cpuct)
+        b.record(st)
+        steps.append((a, b))
+    torch.cuda.synchronize()
+    c1 = sp.mcts.counters()
+    d = {k: c1[k] - c0[k] for k in c1 if k not in ("errors", "nodes", "children")}
+    sel_ms = e_sel[0].elapsed_time(e_sel[1])
+    step_ms = [a.elapsed_time(b) for a, b in steps]
+    eng = sp.eng
+    F = ev.policy_w.shape[1]
+    active = int(sp.active.sum())
+    nbytes = leaf_step_bytes(d, active * n, eng.N, eng.P, eng.W, F)
+    return {"ms_per_sim_step": (sel_ms + sum(step_ms)) / n, "bytes_per_sim_step": nbytes / n,
+            "k_leaf_step_us": 1e3 * sum(step_ms) / n, "k_select_us": 1e3 * sel_ms, "counters": d}
 
 
 def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, warmup: int, rank: int,
@@ -208,12 +260,26 @@ def bench_selfplay(args, world, rank):
         elapsed, sims = float(tmax[0].item()), int(t[1].item())
     steps_sim = args.steps * args.sims  # sim-steps timed (one simulation per tree each)
     obs_bytes = 4 * 2 * eng.P * eng.N * eng.N
-    sbytes = search_bytes(delta, local_sims, obs_bytes, 8 * eng.W)
-    search_ms = ms.get("select", 0.0) + ms.get("expand", 0.0)
-    achieved = sbytes / steps_sim / (search_ms * 1e-3) if search_ms else 0.0
-    net_flops = RESNET_FLOPS_PER_LEAF * delta["expanded"] / steps_sim
-    net_peak = FP32_PEAK if args.nn_dtype == "fp32" else FP16_PEAK
     conv = time_leaf_conv(sp) if args.nn_dtype == "fp32" else None
+    ls = time_leaf_step(sp)
+    if ls is not None:
+        # the search launches of the timed path (k_select + k_leaf_step), timed live
+        search = {"bound": "hbm", "kernel": "k_select (once per ply) + k_leaf_step (per simulation: sparse policy "
+                                            "head, expand/backup, next descent + leaf bitmask/observation)",
+                  "achieved": ls["bytes_per_sim_step"] / (ls["ms_per_sim_step"] * 1e-3) / 1e9,
+                  "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                  "frac": ls["bytes_per_sim_step"] / (ls["ms_per_sim_step"] * 1e-3) / HBM_PEAK, "traffic": None,
+                  "bytes_per_sim_step": ls["bytes_per_sim_step"], "search_ms_per_sim_step": ls["ms_per_sim_step"],
+                  "k_leaf_step_us": ls["k_leaf_step_us"],
+                  "note": "bytes as the kernels move them; the policy-Linear rows (97 MB table) are counted per "
+                          "use and served mostly from the 256 MB Infinity Cache"}
+    else:
+        sbytes = search_bytes(delta, local_sims, obs_bytes, 8 * eng.W)
+        search_ms = ms.get("select", 0.0) + ms.get("expand", 0.0)
+        achieved = sbytes / steps_sim / (search_ms * 1e-3) if search_ms else 0.0
+        search = {"bound": "hbm", "kernel": "k_select+k_expand_backup (search, stage-timed eager ply)",
+                  "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                  "traffic": None, "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms}
     ks = ms.pop("k_sims", None)
     out = {
         "metric": "MCTS sims/sec on 20x20 Blokus (4 players, 256 games/GPU, 100 sims/move)",
@@ -231,17 +297,7 @@ def bench_selfplay(args, world, rank):
         "config": {"workload": "config 3 (N=1) / 4 (N=8): AlphaZero self-play 20x20, 256 concurrent games per GPU, "
                                "100 sims/move, ResNet-5x64 leaf eval", "global_batch": G * world,
                    "parallelism": f"dp{world} (independent games)", "model": args.model},
-        "search_roofline": {"bound": "hbm", "kernel": "k_select+k_expand_backup (search)",
-                            "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                            "frac": achieved / HBM_PEAK, "traffic": None,
-                            "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms},
-        "net_roofline": {"bound": "mfma",
-                         "kernel": "leaf ResNet forward (the leaf-net launch + the sparse policy head); FLOP counted "
-                                   "as the fp32 direct-convolution network (347.5 MFLOP/leaf) against the f32 MFMA "
-                                   "peak: the fp32-equivalent rate",
-                         "achieved": net_flops / (ms.get("net", 1e9) * 1e-3) / 1e12 if ms else None,
-                         "peak": net_peak / 1e12, "unit": "TFLOP/s",
-                         "frac": (net_flops / (ms["net"] * 1e-3)) / net_peak if ms else None},
+        "search_roofline": search,
         "stage_ms_per_sim_step": ms,
         "engine_counters": delta,
     }
