@@ -340,6 +340,22 @@ int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, co
                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
                   const float* w2, const float* b2, int P, float* pf, float* vout, float* out, void* stream);
 
+/* The same leaf ResNet with the residual tower as Winograd F(2x2,3x3) convolutions on split-f16
+ * MFMA products (leafnet_wino.hip): 2.25x fewer matrix products, same fp32-class accuracy. The
+ * stem, heads and arguments as bk_leafnet_x3 except the tower: utower = nlayers x
+ * bk_leafnet_wx3_weight_bytes() bytes of split U = G g G^T in the kernel's fragment order
+ * (nets.py pack_wx3), sutower [nlayers][64] its inverse scales; x0ws [B][N*N][64] f32 device
+ * workspace (the stem output kept for the tower's final residual). N = 20
+ * (bk_leafnet_wx3_supported). Replaces the same reference forward as bk_leafnet_x3
+ * (models/blokus_nnet.py:135-150 via neural_network.py:92-110). */
+int bk_leafnet_wx3_weight_bytes(void);
+int bk_leafnet_wx3_supported(int N);
+int bk_leafnet_wx3(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
+                   int nlayers, const void* utower, const float* sutower, const float* btower, const float* bounds,
+                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t,
+                   const float* b1, const float* w2, const float* b2, int P, float* pf, float* vout, float* x0ws,
+                   float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
