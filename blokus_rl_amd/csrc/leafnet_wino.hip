@@ -56,12 +56,19 @@ __device__ __forceinline__ int wx_sw(int gr, int gc) { return (((gr + 1) >> 1) *
 // (the MFMA B-operand reads of a ds_read_b128 lane group hit 16 distinct bank groups)
 __device__ __forceinline__ int wx_vf(int n) { return (n >> 1) & 7; }
 
-// one MFMA step: acc (+)= ah*bh + al*bh + ah*bl, A operands from AGPRs
+// one MFMA step: acc (+)= ah*bh + al*bh + ah*bl. BK_WX_ASM=1: inline asm with the A operands
+// from AGPRs and a 2-state pad for operands the compiler has just copied in; 0 (default): the
+// builtin (the compiler allocates, pads and schedules)
+#ifndef BK_WX_ASM
+#define BK_WX_ASM 0
+#endif
 template <bool INIT>
 __device__ __forceinline__ void wx_mfma(f32x4& acc, const h16x8& ah, const h16x8& al, const h16x8& bh,
                                         const h16x8& bl) {
+#if BK_WX_ASM
   if (INIT)
     asm volatile(
+        "s_nop 1\n\t"
         "v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\t"
         "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
         "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
@@ -69,11 +76,18 @@ __device__ __forceinline__ void wx_mfma(f32x4& acc, const h16x8& ah, const h16x8
         : "a"(ah), "v"(bh), "a"(al), "v"(bl));
   else
     asm volatile(
+        "s_nop 1\n\t"
         "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
         "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
         "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
         : "+v"(acc)
         : "a"(ah), "v"(bh), "a"(al), "v"(bl));
+#else
+  f32x4 c = INIT ? f32x4{0.f, 0.f, 0.f, 0.f} : acc;
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+#endif
 }
 
 __device__ __forceinline__ f32x4 relu4(f32x4 y) {
@@ -431,8 +445,10 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_wx3(const float* __re
             // three slots back: that quarter's accumulators are final (48 MFMAs since)
             const int qp = wx_q((qi + 1) & 3);
             if (tg > 0 || qi == 3) {
+#if BK_WX_ASM
 #pragma unroll
               for (int x = 0; x < 4; ++x) asm volatile("" : "+v"(acc[qp][x]));
+#endif
               partial(qp);
             }
           }
@@ -441,12 +457,14 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_wx3(const float* __re
       }
     }
     // tail: the last group's quarters 1..3 (slots 25..27), its outputs, the next conv's last U quarter
+#if BK_WX_ASM
     // the MFMA writes of the last slots -> VALU reads (hipcc does not see the asm MFMAs' latency)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int x = 0; x < 4; ++x) asm volatile("" : "+v"(acc[q][x]));
+#endif
     partial(wx_q(1));
     partial(wx_q(2));
     partial(wx_q(3));
