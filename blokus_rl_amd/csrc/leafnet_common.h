@@ -141,6 +141,26 @@ __device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {
   return r;
 }
 
+__device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// 4-wide adds / subtracts as two packed f32 ops (the compiler emits four v_sub_f32 for f32x4)
+__device__ __forceinline__ f32x4 add4(f32x4 a, f32x4 b) {
+  const f32x2 lo = pk_add(f32x2{a.x, a.y}, f32x2{b.x, b.y}), hi = pk_add(f32x2{a.z, a.w}, f32x2{b.z, b.w});
+  return f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+__device__ __forceinline__ f32x4 sub4(f32x4 a, f32x4 b) {
+  const f32x2 lo = pk_sub(f32x2{a.x, a.y}, f32x2{b.x, b.y}), hi = pk_sub(f32x2{a.z, a.w}, f32x2{b.z, b.w});
+  return f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+__device__ __forceinline__ f32x4 fma4(f32x4 a, f32x4 b, f32x4 c) {
+  const f32x2 lo = pk_fma(f32x2{a.x, a.y}, f32x2{b.x, b.y}, f32x2{c.x, c.y});
+  const f32x2 hi = pk_fma(f32x2{a.z, a.w}, f32x2{b.z, b.w}, f32x2{c.z, c.w});
+  return f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+
 // max(m, |a|, |b|) in one VALU op (fmaxf would canonicalize every input first)
 __device__ __forceinline__ float max3_abs(float m, float a, float b) {
   float r;

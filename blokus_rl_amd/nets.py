@@ -298,13 +298,21 @@ def pack_x3(w: torch.Tensor, b: torch.Tensor | None = None) -> tuple[torch.Tenso
     return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous(), bound.to(w.device)
 
 
+def wx3_channel(ks: int, ch: int, e: int) -> int:
+    """bk_leafnet_wx3's K order: element e of k-group ks in K chunk ch is input channel
+    4 * slot + e % 4 with slot = 8 (ks & 1) + 4 (ks >> 1) + 2 ch + e // 4 (leafnet_wino.hip
+    wx_slot: the bank-conflict-free grid slots of the window reads)."""
+    return 4 * (8 * (ks & 1) + 4 * (ks >> 1) + 2 * ch + e // 4) + e % 4
+
+
 def pack_wx3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """[64, 64, 3, 3] tower conv weights -> bk_leafnet_wx3's operands: (the Winograd F(2x2,3x3) U =
     G w G^T, computed in fp64, scaled per output channel by 2^e_o so that its largest magnitude
     over (channel, position) lies in [2^14, 2^15) and split hi = f16(x), lo = f16(x - hi), as
-    uint8 bytes; inverse scales 2^-e_o f32 [64]). Fragment order [xi1 4][xi2 4][chunk 2][wave 4]
-    [part hi/lo][lane 64][8 f16]: lane l of wave w holds U[16w + l%16][32 chunk + 8 (l/16) .. +7]
-    at position (xi1, xi2) — the A operand of v_mfma_f32_16x16x32_f16."""
+    uint8 bytes; inverse scales 2^-e_o f32 [64]). Fragment order [xi1 4][m 4][xi2 4][chunk 2]
+    [part hi/lo][lane 64][8 f16]: wave xi1, lane l = 16 ks + r holds U[16 m + r][wx3_channel(ks,
+    chunk, e)] at (xi1, xi2), e = 0..7 — the A operand of v_mfma_f32_16x16x32_f16 for output
+    block m."""
     assert w.shape == (64, 64, 3, 3)
     G = torch.tensor(_WINO_G, dtype=torch.float64)
     U = torch.einsum("ik,ockl,jl->ocij", G, w.detach().to("cpu", torch.float64), G)  # [o][c][xi1][xi2]
@@ -315,8 +323,17 @@ def pack_wx3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     hi = scaled.to(torch.float16)
     lo = (scaled - hi.to(torch.float64)).to(torch.float16)
     parts = torch.stack([hi, lo])                                 # [part][o][c][xi1][xi2]
-    parts = parts.view(2, 4, 16, 2, 4, 8, 4, 4)                   # [part][wave][row][chunk][kgroup][8][xi1][xi2]
-    packed = parts.permute(6, 7, 3, 1, 0, 4, 2, 5).contiguous()   # [xi1][xi2][chunk][wave][part][kgroup][row][8]
+    chan = torch.tensor([[[wx3_channel(ks, ch, el) for el in range(8)] for ks in range(4)] for ch in range(2)])
+    q = torch.arange(4).view(4, 1, 1, 1, 1, 1, 1, 1)
+    m = torch.arange(4).view(1, 4, 1, 1, 1, 1, 1, 1)
+    x = torch.arange(4).view(1, 1, 4, 1, 1, 1, 1, 1)
+    ch = torch.arange(2).view(1, 1, 1, 2, 1, 1, 1, 1)
+    pt = torch.arange(2).view(1, 1, 1, 1, 2, 1, 1, 1)
+    ks = torch.arange(4).view(1, 1, 1, 1, 1, 4, 1, 1)
+    r = torch.arange(16).view(1, 1, 1, 1, 1, 1, 16, 1)
+    el = torch.arange(8).view(1, 1, 1, 1, 1, 1, 1, 8)
+    c = chan[ch, ks, el]                                          # broadcast to the full index shape
+    packed = parts[pt, 16 * m + r, c, q, x].contiguous()          # [q][m][xi2][ch][part][ks][r][8]
     inv = torch.pow(2.0, -e).to(torch.float32)
     return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous()
 

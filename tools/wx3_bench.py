@@ -8,8 +8,8 @@ import torch
 sys.path.insert(0, ".")
 from blokus_rl_amd.nets import LeafResNet, ResNet, leafnet_wx3, leafnet_x3  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+B = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else 256
+reps = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else 50
 torch.manual_seed(0)
 net = ResNet(20, 4, 30433, 5).cuda().eval()
 leaf = LeafResNet(net, normalize=False, features=True).eval()
@@ -32,3 +32,29 @@ pf2, v2 = leafnet_wx3(obs, leaf)
 out["max_abs_diff_pf"] = float((pf1 - pf2).abs().max())
 out["max_abs_diff_v"] = float((v1 - v2).abs().max())
 print(json.dumps(out))
+
+if "--stamps" in sys.argv:
+    import ctypes
+
+    import numpy as np
+
+    from blokus_rl_amd.engine import load_library
+
+    lib = load_library()
+    lib.bk_wx_stamps.argtypes = [ctypes.c_void_p]
+    leafnet_wx3(obs, leaf)
+    torch.cuda.synchronize()
+    s = np.zeros(256 * 4 * 64, dtype=np.uint64)
+    assert lib.bk_wx_stamps(s.ctypes.data_as(ctypes.c_void_p)) == 0
+    s = s.reshape(256, 4, 64).astype(np.int64)[:B]
+    rel = s - s[:, :, 0:1]
+    med = lambda x: float(np.median(x))  # noqa: E731
+    grp = []
+    for tg in range(7):
+        a, w, y = 2 + 3 * tg, 3 + 3 * tg, 4 + 3 * tg
+        prev = rel[:, :, 1] if tg == 0 else rel[:, :, 1 + 3 * tg]
+        grp.append({"phaseA": med(rel[:, :, a] - prev) if tg else None, "barrier+R": med(rel[:, :, w] - rel[:, :, a]),
+                    "phaseB": med(rel[:, :, y] - rel[:, :, w])})
+    res = {"prologue": med(rel[:, :, 1]), "layer1_groups": grp, "layer1": med(rel[:, :, 30] - rel[:, :, 2] + (rel[:, :, 5] - rel[:, :, 4])),
+           "total": med(rel[:, :, 31])}
+    print(json.dumps(res))
