@@ -26,3 +26,14 @@ def state_of(b64: str) -> np.ndarray:
 
 def unhex(xs):
     return [float.fromhex(x) for x in xs]
+
+
+def load_episodes():
+    """tests/golden/selfplay_golden.json: reference trainer._self_play episodes
+    (make_selfplay_golden.py)."""
+    with open(os.path.join(GOLDEN, "selfplay_golden.json"), encoding="utf-8") as f:
+        return json.load(f)["episodes"]
+
+
+def pi_of(b64: str) -> np.ndarray:
+    return np.frombuffer(base64.b64decode(b64), dtype=np.float32).copy()

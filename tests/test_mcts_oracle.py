@@ -49,3 +49,51 @@ def test_golden_cases_reach_terminal_leaves():
     if len(TERMINAL_HITS) < len(CASES):
         pytest.skip("run with the parametrized cases")
     assert sum(TERMINAL_HITS.values()) > 0, TERMINAL_HITS
+
+
+EPISODES = None
+
+
+def _episodes():
+    global EPISODES
+    if EPISODES is None:
+        from mcts_golden_util import load_episodes
+        EPISODES = load_episodes()
+    return EPISODES
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_oracle_episode_matches_reference_self_play(k):
+    """A whole reference self-play episode (trainer.py:92-137, golden from
+    make_selfplay_golden.py) restated over MCTSOracle: the same legacy np.random stream
+    (np.random.seed, Dirichlet(1) root noise at weight 0.25, np.random.choice on the float32
+    pi) gives the same actions, bit-identical float32 pi per ply and the same final scores."""
+    from mcts_golden_util import pi_of
+    ep = _episodes()[k]
+    o = Oracle(*ep["preset"])
+
+    def evaluate(s, player):
+        ids = o.legal_ids(s, player)
+        p, v = prior_value(o.hash(s), len(ids), o.P)
+        return ids, p, v.astype(np.float64)
+
+    m = MCTSOracle(o, evaluate)
+    np.random.seed(ep["seed"])
+    s = o.init_state()
+    root = True
+    for ply, a_ref in enumerate(ep["actions"]):
+        assert o.game_ended(s) is None
+        for _ in range(ep["sims"]):
+            m.simulate(s, cpuct=ep["cpuct"])
+        ids, d = m.get_distribution(s, ep["temperature"])
+        if root:
+            noise = np.random.dirichlet(np.array(1 * np.ones_like(d.astype(np.float32))))
+            d = d * 0.75 + noise * 0.25
+            root = False
+        pi = d.astype(np.float32)
+        assert len(ids) == ep["K"][ply] == len(o.legal_ids(s))
+        assert pi.tobytes() == pi_of(ep["pi"][ply]).tobytes(), f"ply {ply}"
+        a = int(ids[np.random.choice(len(d), p=pi)])
+        assert a == a_ref, f"ply {ply}"
+        s, _ = o.next_state(s, a)
+    assert o.game_ended(s).tolist() == ep["z"]

@@ -119,3 +119,72 @@ def test_selfplay_raises_when_root_exceeds_cap():
     sp = SelfPlay(eng, DumbNet(7, 2, eng.A), 4, num_sims=4, cap=8, seed=3)  # 7x7 first move: > 8 ids
     with pytest.raises(EngineError):
         sp.run(2)
+
+
+def test_play_ply_sampling_statistics():
+    """SelfPlay.play_ply's sampling against the reference episode's law (trainer.py:108-135):
+    on the first ply pi = 0.75 pi_search + 0.25 Dir(1) (one noise draw per game), the action is a
+    draw from that pi; later plies carry no noise; z is each game's final scores. 2048 games from
+    the same root with a deterministic net share pi_search (a weight-0 twin gives it), so
+      * every game's implied noise is a Dirichlet(1) point: >= 0, sums to 1 on the K legal ids,
+        each coordinate Beta(1, K-1) (Kolmogorov-Smirnov, p > 1e-4);
+      * first-ply action counts match sum_g pi_g (chi-square, p > 1e-4);
+      * games that took the same first action have bit-identical second-ply pi (no noise);
+      * z_table[g] = the oracle's scores of game g's final state."""
+    from scipy import stats as st
+
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import DumbNet
+
+    eng = Engine(7, 2, 5)
+    o = Oracle(7, 2, 5)
+    G = 2048
+    torch.manual_seed(0)
+    net = DumbNet(7, 2, eng.A).to(eng.device).eval()
+    sp = SelfPlay(eng, net, G, num_sims=8, seed=11)
+    twin = SelfPlay(eng, net, G, num_sims=8, seed=12, dirichlet_weight=0.0)
+    twin.play_ply()
+    sp.run(60)
+    assert sp.stats.games_finished == G
+
+    k0 = int(sp._records[0][3][0].item())
+    ids0 = sp._records[0][1][0, :k0].long().cpu().numpy()
+    s0 = sp._records[0][0][0].cpu().numpy()
+    assert (ids0 == o.legal_ids(s0)).all()
+    base = twin._records[0][2][:, :k0].double().cpu().numpy()
+    assert (base == base[0]).all()  # one search result for every game
+    pi0 = sp._records[0][2].double().cpu().numpy()
+    assert (pi0[:, k0:] == 0).all()
+    noise = (pi0[:, :k0] - 0.75 * base[0]) / 0.25
+    assert noise.min() > -1e-5 and np.abs(noise.sum(1) - 1).max() < 1e-5
+    beta = st.beta(1, k0 - 1)
+    for j in (0, k0 // 2, k0 - 1):
+        assert st.kstest(np.clip(noise[:, j], 0, 1), beta.cdf).pvalue > 1e-4, j
+
+    # first-ply actions, read back from the second-ply roots
+    child = {o.hash(o.next_state(s0, int(a))[0]): i for i, a in enumerate(ids0)}
+    s1 = sp._records[1][0].cpu().numpy()
+    pick = np.array([child[o.hash(s1[g])] for g in range(G)])
+    obs = np.bincount(pick, minlength=k0).astype(np.float64)
+    exp = pi0[:, :k0].sum(0)
+    big = exp >= 5
+    f_obs = np.append(obs[big], obs[~big].sum())
+    f_exp = np.append(exp[big], exp[~big].sum())
+    if f_exp[-1] < 5:
+        f_obs, f_exp = f_obs[:-1], f_exp[:-1]
+    f_exp *= f_obs.sum() / f_exp.sum()
+    assert st.chisquare(f_obs, f_exp).pvalue > 1e-4
+
+    # no noise after the first ply: same first action -> same tree -> same pi
+    pi1 = sp._records[1][2].cpu().numpy()
+    for i in np.unique(pick):
+        rows = pi1[pick == i]
+        assert (rows == rows[0]).all(), i
+
+    z = sp.z_table[:G].cpu().numpy()
+    fin = sp.roots.cpu().numpy()
+    for g in range(0, G, 7):
+        assert o.game_ended(fin[g]).tolist() == z[g].tolist(), g
+    ex = sp.examples()
+    assert set(map(tuple, ex.z.cpu().numpy().tolist())) <= set(map(tuple, z.tolist()))
