@@ -138,6 +138,74 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step(DevPreset dp, Dev
 #undef BK_STEP_STAMP
 }
 
+// k_leaf_step with the expansion overlapped (the default; BK_STEP_OVERLAP=0 keeps k_leaf_step).
+// After the logit prologue (all waves: the leaf bitmask compacted, the features in LDS), wave 0
+// publishes the new node (table entry, child range), backs the value up and — when do_select —
+// descends for the next simulation at once, while waves 1.. compute the logits into LDS; the last
+// of them to finish writes the new node's children (softmax + init) and releases a flag. The
+// descent waits on that flag only if it reaches the new node before its children are stored
+// (its children's P are the only data it can need from the other waves). Then all waves build the
+// next leaf's bitmask and observation. The logits, priors, backup and descent are expand_tree's
+// and select_descend's in the same order, so the trees are bitwise those of the per-stage
+// launches; what goes is the wait of the expansion and descent for the slowest logit wave.
+// lds = [W32pad mask | kLeafCap ids | F features | kLeafCap logits] then, at sel_off, the
+// descent's [state | 2 kMaxN | W32pad].
+__global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, DevMcts m, const float* __restrict__ feat,
+                                                                    int64_t ldf, int F, const float* __restrict__ W,
+                                                                    const float* __restrict__ bias,
+                                                                    const float* __restrict__ values, int do_select,
+                                                                    const uint32_t* __restrict__ roots,
+                                                                    const int32_t* __restrict__ active, double cpuct,
+                                                                    int32_t* __restrict__ status_out,
+                                                                    float* __restrict__ obs,
+                                                                    uint64_t* __restrict__ mask_out, int sel_off) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ int status_sh;
+  __shared__ StepExpand sx;
+  const int t = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x == 0) {
+    sx.ready = 0;
+    sx.pready = 0;
+    sx.done = 0;
+    status_sh = 0;
+  }
+  __syncthreads();
+  const int K = leaf_logits_prologue(dp, m, t, 0, feat, ldf, F, lds);
+  const bool logits = K >= 0 && K <= kLeafCap;  // block-uniform
+  const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
+  float* lg = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap + F);
+  uint32_t* lsel = lds + sel_off;
+  if (wave == 0) {
+    expand_head_backup(m, t, dp.P, K, values, &sx);
+    if (do_select) {
+      // this wave's table entry and backup stores, visible to its own descent loads
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      asm volatile("buffer_inv sc0" ::: "memory");
+      const int err = readlane_i(lane_id() == 0 ? sx.err : 0, 0);
+      const int64_t pend = (logits && err == 0) ? (int64_t)sx.off : -1;
+      const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lsel, pend, &sx.pready);
+      if (lane_id() == 0) status_sh = st;
+    }
+  } else if (logits) {
+    leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg);
+    int done = 0;
+    if (lane_id() == 0) done = __hip_atomic_fetch_add(&sx.done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    done = readlane_i(done, 0);
+    if (done == kStepWaves - 2) {  // the last logit wave: every logit is in LDS
+      while (__hip_atomic_load(&sx.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      const int err = readlane_i(sx.err, 0);
+      if (err == 0) expand_children_lds(m, (int64_t)sx.off, K, ids, lg);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the children stored before the flag
+      if (lane_id() == 0) __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  if (!do_select) return;
+  select_leaf<kStepWaves>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
+}
+
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
   if (e == 1.0 || n <= 1u) return (double)n;
   return pow((double)n, e);
@@ -337,6 +405,16 @@ int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const f
   BK_REQUIRE(((uintptr_t)W & 15u) == 0 || (F & 3) != 0, "bk_mcts_leaf_step: W must be 16-byte aligned");
   BK_REQUIRE(!do_select || (roots && leaf_status && obs), "bad argument: select outputs");
   const DevPreset& dp = m->ctx->dp;
+  const char* ov = getenv("BK_STEP_OVERLAP");  // read per call (graph capture reads it once)
+  const int overlap = ov ? atoi(ov) : 1;
+  if (overlap) {
+    const int sel_off = (int)(((size_t)dp.W32pad + 2 * kLeafCap + F + 3) & ~(size_t)3);
+    const size_t words = (size_t)sel_off + kStateWords + 2 * kMaxN + dp.W32pad;
+    hipLaunchKernelGGL(k_leaf_step_ov, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
+                       (hipStream_t)stream, dp, m->d, feat, ldf, F, W, bias, values, do_select,
+                       (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, sel_off);
+    return launch_check("k_leaf_step_ov");
+  }
   size_t words = (size_t)dp.W32pad + kLeafCap + F;                               // leaf logits
   words = std::max(words, (size_t)dp.W32pad + kExpandLdsIds);                    // expand
   words = std::max(words, (size_t)(kStateWords + 2 * kMaxN + dp.W32pad));       // select

@@ -208,9 +208,17 @@ __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K
 // terminal board, the path recorded (mcts.py:37-50); the leaf state stays in LDS for select_leaf.
 // lds = kStateWords + 2 kMaxN + W32pad words. Returns the leaf status (wave-uniform): 0 inactive
 // tree or error, 1 a leaf for the net, 2 a terminal board.
+// pend_off / pend_flag (k_leaf_step_ov): the children of the node at child offset pend_off are
+// still being written by another wave of the workgroup; the descent waits for pend_flag (set with
+// release semantics once they are stored) before it reads them.
+__device__ __forceinline__ void wait_flag_acquire(int* flag) {
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+  asm volatile("buffer_inv sc0" ::: "memory");
+}
 __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts& m, int t,
                                               const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
-                                              double cpuct, int32_t* __restrict__ status_out, uint32_t* lds) {
+                                              double cpuct, int32_t* __restrict__ status_out, uint32_t* lds,
+                                              int64_t pend_off = -1, int* pend_flag = nullptr) {
   uint32_t* s = lds;
   uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
   const int l = lane_id();
@@ -250,6 +258,10 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     BK_TACC(t_probe, found = table_find(m, t, table_key(s), off, Kn, nullptr));
     if (!found) break;
     if (Kn <= 0) { err |= kErrIllegal; break; }  // a stored node always has a legal move
+    if (off == pend_off) {
+      wait_flag_acquire(pend_flag);
+      pend_off = -1;
+    }
     scanned += Kn;
     int a, ci;
     BK_TACC(t_child, ci = select_child(m, off, Kn, cp, a));
@@ -367,18 +379,18 @@ __device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m
 // kLeafBlocks workgroups per tree each compact the leaf bitmask (ascending ids) and take a
 // contiguous share of the ids; a wave computes four dot products at a time (16 lanes each) over
 // the feature row staged in LDS, W rows read as coalesced float4s, several loads in flight.
-// k_leaf_logits' work on tree t by a workgroup of any multiple of 64 threads, share c of nc, R x 4
-// ids per wave at a time (k_sims: the whole tree, nc 1, R 2): lds = W32pad + kLeafCap + F words.
-template <int R = 1>
-__device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevMcts& m, int t, int c, int nc,
-                                                 const float* __restrict__ feat, int64_t ldf, int F,
-                                                 const float* __restrict__ W, const float* __restrict__ bias,
-                                                 uint32_t* lds) {
+//
+// The leaf's legal ids and feature row into LDS (all threads of the workgroup; two barriers):
+// lds = W32pad mask words | kLeafCap ids | F features. Returns K (also stored to leaf_K when c is
+// 0), or -1 when tree t has no leaf for the net (block-uniform; no barrier taken then).
+__device__ __forceinline__ int leaf_logits_prologue(const DevPreset& dp, const DevMcts& m, int t, int c,
+                                                    const float* __restrict__ feat, int64_t ldf, int F,
+                                                    uint32_t* lds) {
   uint32_t* m32 = lds;                                                   // W32pad words
   int32_t* ids = reinterpret_cast<int32_t*>(lds + dp.W32pad);            // kLeafCap
   float* f = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap);       // F (16-B aligned: W32pad % 4 == 0)
   __shared__ int Ksh;
-  if (m.leaf_status[t] != 1) return;  // block-uniform: no leaf to evaluate
+  if (m.leaf_status[t] != 1) return -1;  // block-uniform: no leaf to evaluate
   const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
   for (int j = threadIdx.x; j < dp.W64; j += blockDim.x) {
     const uint64_t w = lm[j];
@@ -399,11 +411,19 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
     m.leaf_K[t] = K;
     if (K > kLeafCap) atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrLeafCap);
   }
-  if (K > kLeafCap) return;
-  const int lo = (int)((int64_t)K * c / nc), hi = (int)((int64_t)K * (c + 1) / nc);
-  int32_t* out_ids = m.leaf_ids + (size_t)t * kLeafCap;
-  float* out_lg = m.leaf_logit + (size_t)t * kLeafCap;
-  const int nw = blockDim.x >> 6;
+  return K;
+}
+
+// The logits of ids [lo, hi) of the prologue's LDS id list by wave `wave` of nw: logit j to
+// out_lg[j] (global or LDS), its id to out_ids[j] when out_ids is given. Every logit is summed in
+// the same order whichever wave takes it, so any wave split gives the same values, bitwise.
+template <int R = 1>
+__device__ __forceinline__ void leaf_logits_dots(const DevPreset& dp, int lo, int hi, int wave, int nw,
+                                                 const float* __restrict__ W, const float* __restrict__ bias, int F,
+                                                 const uint32_t* lds, int32_t* out_ids, float* out_lg) {
+  const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
+  const float* f = reinterpret_cast<const float*>(lds + dp.W32pad + kLeafCap);
+  const int l = threadIdx.x & 63;
   if (R > 1 && (F & 3) == 0 && F <= 64 * kLeafQ) {
     // R x four ids per wave at a time, 16 lanes each: a lane holds every 16th float4 of each of its
     // R rows (<= kLeafQ a row), all loads issued before the first is used — one memory round trip
@@ -443,7 +463,7 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
 #pragma unroll
         for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
         if (sub == 0 && jr[u] < hi) {
-          out_ids[jr[u]] = idr[u];
+          if (out_ids) out_ids[jr[u]] = idr[u];
           out_lg[jr[u]] = a + bias[idr[u]];
         }
       }
@@ -477,7 +497,7 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
 #pragma unroll
       for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
       if (sub == 0 && ok) {
-        out_ids[j] = id;
+        if (out_ids) out_ids[j] = id;
         out_lg[j] = a + bias[id];
       }
     }
@@ -489,11 +509,26 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
       for (int q = l; q < F; q += kWave) a += r[q] * f[q];
       a = wave_sum_f(a);
       if (l == 0) {
-        out_ids[j] = id;
+        if (out_ids) out_ids[j] = id;
         out_lg[j] = a + bias[id];
       }
     }
   }
+}
+
+
+// k_leaf_logits' work on tree t by a workgroup of any multiple of 64 threads, share c of nc, R x 4
+// ids per wave at a time (k_sims: the whole tree, nc 1, R 2): lds = W32pad + kLeafCap + F words.
+template <int R = 1>
+__device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevMcts& m, int t, int c, int nc,
+                                                 const float* __restrict__ feat, int64_t ldf, int F,
+                                                 const float* __restrict__ W, const float* __restrict__ bias,
+                                                 uint32_t* lds) {
+  const int K = leaf_logits_prologue(dp, m, t, c, feat, ldf, F, lds);
+  if (K < 0 || K > kLeafCap) return;
+  const int lo = (int)((int64_t)K * c / nc), hi = (int)((int64_t)K * (c + 1) / nc);
+  leaf_logits_dots<R>(dp, lo, hi, (int)(threadIdx.x >> 6), (int)(blockDim.x >> 6), W, bias, F, lds,
+                      m.leaf_ids + (size_t)t * kLeafCap, m.leaf_logit + (size_t)t * kLeafCap);
 }
 
 // prior_mode 0: logp = the net's log-probabilities over all A ids -> masked log-softmax + exp
@@ -654,6 +689,141 @@ __device__ __forceinline__ void expand_tree(const DevPreset& dp, const DevMcts& 
     m.ch_N[ci] = n + 1u;
   }
   BK_STAMP(1, 5);
+}
+
+// ---- k_leaf_step_ov: the expansion split between wave 0 (bookkeeping + backup, then the next
+// descent) and the last wave to finish the leaf logits (the new node's children). Together they do
+// expand_tree's work in prior mode 2 with the same arithmetic in the same order, so the trees are
+// bitwise those of the per-stage launches.
+struct StepExpand {
+  long long off;  // the new node's first child (global child index)
+  int K, err;     // its child count; error flags (nonzero: no children are written)
+  int ready;      // wave 0 published off / K / err
+  int pready;     // the children (id, N, Q, P) are stored
+  int done;       // logit waves finished
+};
+
+// wave 0: expand_tree's loads (1), (2) without the children, the table entry, and the backup (3).
+// K = the prologue's leaf K. Publishes off / K / err (release) before the backup.
+__device__ __forceinline__ void expand_head_backup(const DevMcts& m, int t, int P, int K,
+                                                   const float* __restrict__ values, StepExpand* sx) {
+  __shared__ double vsh[kMaxP];
+  const int l = lane_id();
+  const int status = m.leaf_status[t];
+  const int depth = m.depth[t];
+  const int node = m.tree_nodes[t];
+  const int64_t used = m.tree_children[t];
+  const uint64_t key = table_key(m.leaf_state + (size_t)t * kStateWords);
+  if (status == 0) {
+    if (l == 0) {
+      sx->err = -1;
+      __hip_atomic_store(&sx->ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  const size_t pi = (size_t)t * kMaxDepth + l;
+  const bool on_path = l < depth;  // depth <= kMaxDepth = 96: levels 64.. are handled below
+  const int64_t pchild = on_path ? m.path_child[pi] : 0;
+  const int ppl = on_path ? m.path_pl[pi] : 0;
+  int err = 0;
+  if (status == 1) {
+    const int64_t room = m.child_cap_per_tree - used;
+    if (K > kLeafCap) err |= kErrLeafCap;
+    if (node >= m.node_cap) err |= kErrTable;
+    if (K > room) err |= kErrChildPool;
+    int free_slot = -1;
+    if (!err) {
+      int64_t foff;
+      int fK;
+      if (table_find(m, t, key, foff, fK, &free_slot) || free_slot < 0) err |= kErrTable;
+    }
+    if (!err) {
+      if (l == 0) {
+        TabEntry e;
+        e.key = key;
+        e.off = (uint32_t)used;
+        e.K = K;
+        m.tab[(size_t)t * m.TS + free_slot] = e;
+        m.tree_nodes[t] = node + 1;
+        m.tree_children[t] = used + K;
+        ctr_add(m, t, kCtrExpanded, 1ull);
+        ctr_add(m, t, kCtrLeafK, (unsigned long long)K);
+      }
+    } else if (l == 0) {
+      atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
+    }
+    if (l < P) vsh[l] = (double)values[(size_t)t * P + l];
+  } else {
+    if (l < P) vsh[l] = m.leaf_scores[(size_t)t * kMaxP + l];
+  }
+  if (l == 0) {
+    sx->off = (long long)((int64_t)t * m.child_cap_per_tree + used);
+    sx->K = K;
+    sx->err = status == 1 ? err : -1;
+    __hip_atomic_store(&sx->ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  wave_lds_sync();
+  if (on_path) {
+    const double v = vsh[ppl];
+    const uint32_t n = m.ch_N[pchild];
+    const double q = m.ch_Q[pchild];
+    m.ch_Q[pchild] = ((double)n * q + v) / (double)(n + 1u);
+    m.ch_N[pchild] = n + 1u;
+  }
+  for (int d = l + kWave; d < depth; d += kWave) {  // levels 64..kMaxDepth-1 (never at 20x20)
+    const size_t pd = (size_t)t * kMaxDepth + d;
+    const int64_t ci = m.path_child[pd];
+    const double v = vsh[m.path_pl[pd]];
+    const uint32_t n = m.ch_N[ci];
+    const double q = m.ch_Q[ci];
+    m.ch_Q[ci] = ((double)n * q + v) / (double)(n + 1u);
+    m.ch_N[ci] = n + 1u;
+  }
+}
+
+// The new node's children from the logits in LDS (ids[i], lg[i], i < K), by one wave:
+// expand_tree's softmax (prior mode 2) and child initialisation, term for term.
+__device__ __forceinline__ void expand_children_lds(const DevMcts& m, int64_t off, int K, const int32_t* ids,
+                                                    const float* lg) {
+  const int l = lane_id();
+  float x[kGatherRegs];
+  int32_t xid[kGatherRegs];
+#pragma unroll
+  for (int j = 0; j < kGatherRegs; ++j) {
+    const int i = l + j * kWave;
+    const bool ok = i < K;
+    x[j] = ok ? lg[i] : -INFINITY;
+    xid[j] = ok ? ids[i] : 0;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < kGatherRegs; ++j) mx = fmaxf(mx, x[j]);
+  for (int i = l + kGatherRegs * kWave; i < K; i += kWave) mx = fmaxf(mx, lg[i]);
+  mx = wave_max_f(mx);
+  float sum = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kGatherRegs; ++j) sum += l + j * kWave < K ? expf(x[j] - mx) : 0.0f;
+  for (int i = l + kGatherRegs * kWave; i < K; i += kWave) sum += expf(lg[i] - mx);
+  sum = wave_sum_f(sum);
+  const float lse = logf(sum);
+#pragma unroll
+  for (int j = 0; j < kGatherRegs; ++j) x[j] = expf((x[j] - mx) - lse);
+#pragma unroll
+  for (int j = 0; j < kGatherRegs; ++j) {
+    const int i = l + j * kWave;
+    if (i < K) {
+      m.ch_id[off + i] = xid[j];
+      m.ch_N[off + i] = 0u;
+      m.ch_Q[off + i] = 0.0;
+      m.ch_P[off + i] = x[j];
+    }
+  }
+  for (int i = l + kGatherRegs * kWave; i < K; i += kWave) {
+    m.ch_id[off + i] = ids[i];
+    m.ch_N[off + i] = 0u;
+    m.ch_Q[off + i] = 0.0;
+    m.ch_P[off + i] = expf((lg[i] - mx) - lse);
+  }
 }
 
 }  // namespace bk

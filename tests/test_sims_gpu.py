@@ -51,11 +51,13 @@ def test_fused_simulations_match_stagewise(N, T, sims, monkeypatch):
     assert torch.equal(s1[a], s2[a]) and torch.equal(d1, d2)
 
 
-@pytest.mark.parametrize("N,T,sims", [(20, 12, 9), (14, 7, 6)])
-def test_leaf_step_matches_stagewise(N, T, sims):
-    """bk_mcts_leaf_step (policy head + expand/backup + the next descent in one launch) against
-    k_leaf_logits -> k_expand_backup -> k_select: the same trees, counters, leaf states and
-    observations, bitwise."""
+@pytest.mark.parametrize("N,T,sims,overlap", [(20, 12, 9, "1"), (20, 12, 9, "0"), (14, 7, 6, "1"), (20, 64, 40, "1")])
+def test_leaf_step_matches_stagewise(N, T, sims, overlap, monkeypatch):
+    """bk_mcts_leaf_step (policy head + expand/backup + the next descent in one launch; overlap 1
+    = k_leaf_step_ov, the default, whose wave 0 backs up and descends while the other waves
+    compute the logits) against k_leaf_logits -> k_expand_backup -> k_select: the same trees,
+    counters, leaf states and observations, bitwise."""
+    monkeypatch.setenv("BK_STEP_OVERLAP", overlap)
     from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
     from blokus_rl_amd.boards import random_boards
     from blokus_rl_amd.engine import Engine
@@ -65,7 +67,7 @@ def test_leaf_step_matches_stagewise(N, T, sims):
     roots = random_boards(eng, T, seed0=11, max_plies=24 if N == 20 else 12)
     active = torch.ones(T, dtype=torch.int32, device=eng.device)
     active[T // 3] = 0
-    kw = dict(node_cap=64, child_cap=T * 64 * 700)
+    kw = dict(node_cap=sims + 8, child_cap=T * (sims + 8) * 700)
     m1, m2 = BatchedMCTS(eng, T, **kw), BatchedMCTS(eng, T, **kw)
     po = model.f.policy_out
     w, b = po.weight.detach().contiguous(), po.bias.detach().contiguous()
