@@ -168,6 +168,8 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     sx.ready = 0;
     sx.pready = 0;
     sx.done = 0;
+    sx.leaf_ready = 0;
+    sx.slice = 0;
     status_sh = 0;
   }
   __syncthreads();
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
   float* lg = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap + F);
   uint32_t* lsel = lds + sel_off;
+  uint32_t* m32 = lsel + kStateWords + 2 * kMaxN;
   if (wave == 0) {
     expand_head_backup(m, t, dp.P, K, values, &sx);
     if (do_select) {
@@ -185,7 +188,12 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
       const int err = readlane_i(lane_id() == 0 ? sx.err : 0, 0);
       const int64_t pend = (logits && err == 0) ? (int64_t)sx.off : -1;
       const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lsel, pend, &sx.pready);
-      if (lane_id() == 0) status_sh = st;
+      if (st == 1)
+        for (int i = lane_id(); i < dp.W32pad / 4; i += kWave) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (lane_id() == 0) {
+        status_sh = st;
+        __hip_atomic_store(&sx.leaf_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   } else if (logits) {
     leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg);
@@ -201,9 +209,16 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
       if (lane_id() == 0) __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+  if (do_select) {
+    // every wave joins the next leaf's bitmask once it is free and the descent is done: wave 0
+    // usually starts it alone while the logit waves finish
+    while (__hip_atomic_load(&sx.leaf_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+      __builtin_amdgcn_s_sleep(1);
+    if (readlane_i(status_sh, 0) == 1) mask_slices_claim(dp, lsel, m32, &sx.slice);
+  }
   __syncthreads();
   if (!do_select) return;
-  select_leaf<kStepWaves>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
+  select_leaf<kStepWaves, true>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
 }
 
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {

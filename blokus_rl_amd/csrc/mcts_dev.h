@@ -318,7 +318,8 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
 // index; 1 = the descending wave alone): for a leaf (status 1) the mover's legal bitmask (the
 // orientations split over the waves) and the leaf state to global memory, and for every tree
 // the observation rows the net reads (zeros unless status 1). obs and mask_out may be null.
-template <int NW>
+// BUILT: the bitmask is already in LDS (k_leaf_step_ov builds it with mask_slices_claim).
+template <int NW, bool BUILT = false>
 __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& m, int t, int status,
                                             float* __restrict__ obs, uint64_t* __restrict__ mask_out, uint32_t* lds,
                                             int wave) {
@@ -327,7 +328,9 @@ __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& 
   const int l = lane_id(), tid = wave * kWave + l;
   const int obs_len = 2 * dp.P * dp.N * dp.N;
   if (status == 1) {
-    if (NW == 1)
+    if (BUILT)
+      ;
+    else if (NW == 1)
       build_mask_rows(dp, s, (int)s[kWToMove], m32);
     else
       build_mask_rows_wg<(NW > BK_MASK_WPB ? BK_MASK_WPB : NW)>(dp, s, (int)s[kWToMove], m32, wave);
@@ -701,6 +704,8 @@ struct StepExpand {
   int ready;      // wave 0 published off / K / err
   int pready;     // the children (id, N, Q, P) are stored
   int done;       // logit waves finished
+  int leaf_ready; // wave 0's descent is done (status_sh, the leaf state and its zeroed mask in LDS)
+  int slice;      // next leaf-bitmask slice to claim
 };
 
 // wave 0: expand_tree's loads (1), (2) without the children, the table entry, and the backup (3).
@@ -778,6 +783,30 @@ __device__ __forceinline__ void expand_head_backup(const DevMcts& m, int t, int 
     const double q = m.ch_Q[ci];
     m.ch_Q[ci] = ((double)n * q + v) / (double)(n + 1u);
     m.ch_N[ci] = n + 1u;
+  }
+}
+
+// The leaf bitmask of the state in LDS (s; m32 zeroed by the caller) built by whichever waves
+// call this: each claims slices k = 0..BK_MASK_WPB-1 (the orientations O % BK_MASK_WPB == k, the
+// slices of build_mask_rows_wg) from an LDS counter until none is left, ORing into m32. The
+// caller's barrier ends the build.
+__device__ __forceinline__ void mask_slices_claim(const DevPreset& dp, const uint32_t* s, uint32_t* m32, int* counter) {
+  RowCtx c = row_ctx(dp, s, (int)s[kWToMove], m32);
+  for (;;) {
+    // the context opaque per claim: nothing derived from it is hoisted out of the loop (the
+    // compiler would otherwise keep every slice's shifted rows live at once)
+#pragma unroll
+    for (int d = 0; d < 5; ++d) asm volatile("" : "+v"(c.fr[d]), "+v"(c.ar[d]));
+#pragma unroll
+    for (int h = 0; h < 6; ++h) asm volatile("" : "+v"(c.rowok[h]));
+    asm volatile("" : "+v"(c.r), "+v"(c.rN1), "+v"(c.pieces));
+    int k = 0;
+    if (lane_id() == 0) k = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    k = readlane_i(k, 0);
+    if (k >= BK_MASK_WPB) break;
+    DevPreset dq = dp;  // the scalar sizes opaque per claim as well
+    asm volatile("" : "+s"(dq.N), "+s"(dq.num_pieces));
+    orient_dispatch<BK_MASK_WPB>(dq, c, k, std::make_index_sequence<BK_MASK_WPB>{});
   }
 }
 
