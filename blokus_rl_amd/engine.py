@@ -84,6 +84,9 @@ _SIGS = {
     "bk_leafnet_wx3_supported": (_i, [_i]),
     "bk_leafnet_wx3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8
                        + [_i, _vp, _vp, _vp, _vp, _vp]),
+    "bk_leafnet_x3g_supported": (_i, [_i]),
+    "bk_leafnet_x3g": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8
+                       + [_i, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

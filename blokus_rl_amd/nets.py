@@ -345,8 +345,8 @@ def net_math() -> str:
     import os
 
     m = os.environ.get("BK_NET_MATH", "x3")
-    if m not in ("wx3", "x3", "f32"):
-        raise ValueError(f"BK_NET_MATH must be wx3, x3 or f32, got {m!r}")
+    if m not in ("x3g", "wx3", "x3", "f32"):
+        raise ValueError(f"BK_NET_MATH must be x3g, wx3, x3 or f32, got {m!r}")
     return m
 
 
@@ -398,6 +398,33 @@ def leafnet_wx3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
     _check(lib.bk_leafnet_wx3(
         ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
         _ptr(model.wx3_utower), _ptr(model.wx3_sutower), _ptr(model.b_tower), _ptr(model.x3_bounds),
+        *[_ptr(t) for t in h[1:]], P, _ptr(pf), _ptr(v), _ptr(x0),
+        None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
+    return (pf, v, out) if want_out else (pf, v)
+
+
+def leafnet_x3g(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
+    """bk_leafnet_x3g: leafnet_x3's net with the tower convolutions group-major (20x20 boards): the
+    tower output bitwise leafnet_x3's, the heads summed in another order."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, cin, N, _ = obs.shape
+    assert cin == 8 and obs.dtype == torch.float32 and obs.is_contiguous()
+    f = model.f
+    lib = load_library()
+    nl = 2 * len(f.blocks)
+    assert model.x3_wtower.numel() == nl * lib.bk_leafnet_x3_weight_bytes(64)
+    assert model.x3_wstem.numel() == lib.bk_leafnet_x3_weight_bytes(8)
+    P = f.value_fc2.out_features
+    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=obs.device)
+    v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
+    x0 = torch.empty((B, N * N, 64), dtype=torch.float32, device=obs.device)
+    out = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device,
+                      memory_format=torch.channels_last) if want_out else None
+    h = model.x3_heads
+    _check(lib.bk_leafnet_x3g(
+        ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
+        _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), _ptr(model.x3_bounds),
         *[_ptr(t) for t in h[1:]], P, _ptr(pf), _ptr(v), _ptr(x0),
         None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
     return (pf, v, out) if want_out else (pf, v)
@@ -567,6 +594,13 @@ class LeafResNet(nn.Module):
             from .engine import load_library
 
             math = net_math() if self.x3 else "f32"
+            if math == "x3g" and load_library().bk_leafnet_x3g_supported(x.shape[2]):
+                # the whole net in one launch, the tower convs group-major (bk_leafnet_x3g)
+                pf, v = leafnet_x3g(x.float().contiguous(), self)
+                if self.features:
+                    return pf, v
+                logits = f.policy_out(pf)
+                return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
             if math == "wx3" and load_library().bk_leafnet_wx3_supported(x.shape[2]):
                 # the whole net in one launch, the tower as Winograd convs on split-f16 products
                 pf, v = leafnet_wx3(x.float().contiguous(), self)
@@ -574,7 +608,7 @@ class LeafResNet(nn.Module):
                     return pf, v
                 logits = f.policy_out(pf)
                 return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
-            if math in ("x3", "wx3") and load_library().bk_leafnet_x3_supported(x.shape[2]):
+            if math in ("x3", "wx3", "x3g") and load_library().bk_leafnet_x3_supported(x.shape[2]):
                 # the whole net in one launch on split-f16 MFMA products (bk_leafnet_x3)
                 pf, v = leafnet_x3(x.float().contiguous(), self)
                 if self.features:

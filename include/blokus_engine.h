@@ -356,6 +356,21 @@ int bk_leafnet_wx3(const float* obs, int B, int N, int cin, const void* wstem, c
                    const float* b1, const float* w2, const float* b2, int P, float* pf, float* vout, float* x0ws,
                    float* out, void* stream);
 
+/* The same leaf ResNet as bk_leafnet_x3 (same operands: pack_x3 weights, scales, bounds, heads)
+ * with the residual tower's convolutions group-major (leafnet_g.hip): each wave keeps its output
+ * channels' weights for a whole conv in registers and runs the 25 pixel groups one after another,
+ * the epilogue of group g-1 and the delayed grid writes of group g-4 under group g's MFMAs, so no
+ * layer ends in an epilogue with the matrix cores idle. The tower output is bitwise bk_leafnet_x3's;
+ * the heads sum in another order (fp32 rounding). x0ws: device workspace of B x N*N x 64 floats
+ * (the stem output for the final residual). N = 20 (bk_leafnet_x3g_supported). Replaces the same
+ * reference forward (models/blokus_nnet.py:135-150 via neural_network.py:92-110). */
+int bk_leafnet_x3g_supported(int N);
+int bk_leafnet_x3g(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
+                   int nlayers, const void* wtower, const float* stower, const float* btower, const float* bounds,
+                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t,
+                   const float* b1, const float* w2, const float* b2, int P, float* pf, float* vout, float* x0ws,
+                   float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
