@@ -150,6 +150,17 @@ def main():
         out[f"ids20_{i}"] = np.nonzero(mask)[0].astype(np.int32)
         out[f"p20_{i}"] = np.asarray(p, dtype=np.float32)
         out[f"v20_{i}"] = np.asarray(v, dtype=np.float32)
+    # the config-3 net: 5 residual blocks, the same 30433-action predict() path
+    hp20b5 = _HP(num_res_blocks=5, num_channels=128, linear_dim=128, dropout=0.3, lr=1e-3, weight_decay=1e-4,
+                 model_type="resnet")
+    wrapper5 = nw.BlokusNNetWrapper(g20, hp20b5, device="cpu")
+    wrapper5.model.load_state_dict(det_state_dict({k: v.shape for k, v in wrapper5.model.state_dict().items()}))
+    for i, b in enumerate(boards20):
+        mask = np.zeros(o20.A)
+        mask[o20.legal_ids(b)] = 1
+        p, v = wrapper5.predict(o20.observe(b), mask)
+        out[f"p20b5_{i}"] = np.asarray(p, dtype=np.float32)
+        out[f"v20b5_{i}"] = np.asarray(v, dtype=np.float32)
     fp = os.path.join(HERE, "net_golden.npz")
     np.savez_compressed(fp, **out)
     print(fp, os.path.getsize(fp), "bytes;", sorted(out))

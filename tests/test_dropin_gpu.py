@@ -121,8 +121,8 @@ def test_dropin_mcts_matches_reference(k, game20, game7):
         assert list(d0[:, 1]) == unhex(mv["dist_T0"])
 
 
-@pytest.mark.parametrize("math", ["x3", "f32"])
-def test_predict_batch_matches_reference_predict(game20, math, monkeypatch):
+@pytest.mark.parametrize("math,blocks", [("x3", 2), ("f32", 2), ("x3", 5), ("f32", 5)])
+def test_predict_batch_matches_reference_predict(game20, math, blocks, monkeypatch):
     """The device leaf path (BN-folded net in one HIP launch: k_leafnet_x3, or the exact-f32
     kernels with BK_NET_MATH=f32) and the batch-1 predict() drop-in against the reference
     predict() golden rows (make_net_golden.py: the reference module on the CPU in fp32). Both
@@ -135,7 +135,8 @@ def test_predict_batch_matches_reference_predict(game20, math, monkeypatch):
     mng = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mng)
     G = np.load(os.path.join(GOLDEN, "net_golden.npz"))
-    nn = BlokusNNetWrapper(game20, _hp(num_res_blocks=2), device=game20.device)
+    nn = BlokusNNetWrapper(game20, _hp(num_res_blocks=blocks), device=game20.device)
+    sfx = "" if blocks == 2 else "b5"  # golden rows of the 2-block and the config-3 (5-block) net
     sd = nn.model.state_dict()
     nn.model.load_state_dict({k: v.to(game20.device) for k, v in mng.det_state_dict({k: v.shape for k, v in sd.items()}).items()})
     worst = [0.0, 0.0]
@@ -144,15 +145,15 @@ def test_predict_batch_matches_reference_predict(game20, math, monkeypatch):
         lp, v = nn.predict_batch(obs)
         ids = torch.from_numpy(G[f"ids20_{i}"]).long().to(game20.device)
         p = torch.softmax(lp[0, ids].double(), dim=0).cpu().numpy()
-        pg = G[f"p20_{i}"].astype(np.float64)
+        pg = G[f"p20{sfx}_{i}"].astype(np.float64)
         worst[0] = max(worst[0], float(np.max(np.abs(p - pg) / pg)))
-        worst[1] = max(worst[1], float(np.max(np.abs(v[0].cpu().numpy() - G[f"v20_{i}"]))))
+        worst[1] = max(worst[1], float(np.max(np.abs(v[0].cpu().numpy() - G[f"v20{sfx}_{i}"]))))
         np.testing.assert_allclose(p, pg, rtol=1e-5, atol=1e-9)
-        np.testing.assert_allclose(v[0].cpu().numpy(), G[f"v20_{i}"], atol=1e-5)
+        np.testing.assert_allclose(v[0].cpu().numpy(), G[f"v20{sfx}_{i}"], atol=1e-5)
         pr, vr = nn.predict(G[f"obs20_{i}"], np.isin(np.arange(30433), G[f"ids20_{i}"]).astype(np.float64))
         np.testing.assert_allclose(pr, pg, rtol=1e-5, atol=1e-9)
-        np.testing.assert_allclose(vr, G[f"v20_{i}"], atol=1e-5)
-    print(f"predict {math}: max rel err p {worst[0]:.2e}, max abs err v {worst[1]:.2e}")
+        np.testing.assert_allclose(vr, G[f"v20{sfx}_{i}"], atol=1e-5)
+    print(f"predict {math} blocks={blocks}: max rel err p {worst[0]:.2e}, max abs err v {worst[1]:.2e}")
 
 
 def test_arena_and_players_7x7(game7):

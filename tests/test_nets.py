@@ -48,17 +48,21 @@ class _Game:
         return 30433
 
 
-def test_predict_matches_reference_20x20():
+@pytest.mark.parametrize("blocks", [2, 5])
+def test_predict_matches_reference_20x20(blocks):
+    """The drop-in predict() on the CPU (the same module structure as the reference, fp32) against
+    the reference predict() golden rows, 2-block and config-3 (5-block) nets, at fp32 rounding."""
     from blokus_rl_amd.neural_network import BlokusNNetWrapper
-    hp = types.SimpleNamespace(model_type="resnet", num_res_blocks=2, lr=1e-3, weight_decay=1e-4)
+    hp = types.SimpleNamespace(model_type="resnet", num_res_blocks=blocks, lr=1e-3, weight_decay=1e-4)
     w = BlokusNNetWrapper(_Game(), hp, device="cpu")
     _load(w.model)
+    sfx = "" if blocks == 2 else "b5"
     for i in range(3):
         mask = np.zeros(30433)
         mask[G[f"ids20_{i}"]] = 1
         p, v = w.predict(G[f"obs20_{i}"], mask)
-        np.testing.assert_allclose(p, G[f"p20_{i}"], rtol=1e-4, atol=1e-7)
-        np.testing.assert_allclose(v, G[f"v20_{i}"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(p, G[f"p20{sfx}_{i}"], rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(v, G[f"v20{sfx}_{i}"], rtol=0, atol=1e-6)
 
 
 def test_vectorised_loss_equals_reference_loop():
