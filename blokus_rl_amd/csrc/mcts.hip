@@ -164,6 +164,14 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   __shared__ StepExpand sx;
   const int t = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef BK_STAMPS
+  // diag: 0 start, 1 prologue done, 2 wave 0 backup done, 3 wave 0 descent done, 4 the last logit
+  // wave done, 5 its children stored, 6 the next leaf's bitmask done (all waves), 7 end
+#define BK_OV_STAMP(i) \
+  do { if (lane_id() == 0 && do_select && t < 4096) g_step_stamps[t][i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BK_OV_STAMP(i) do { } while (0)
+#endif
   if (threadIdx.x == 0) {
     sx.ready = 0;
     sx.pready = 0;
@@ -172,8 +180,10 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     sx.slice = 0;
     status_sh = 0;
   }
+  if (wave == 0) BK_OV_STAMP(0);
   __syncthreads();
   const int K = leaf_logits_prologue(dp, m, t, 0, feat, ldf, F, lds);
+  if (wave == 0) BK_OV_STAMP(1);
   const bool logits = K >= 0 && K <= kLeafCap;  // block-uniform
   const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
   float* lg = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap + F);
@@ -181,6 +191,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   uint32_t* m32 = lsel + kStateWords + 2 * kMaxN;
   if (wave == 0) {
     expand_head_backup(m, t, dp.P, K, values, &sx);
+    BK_OV_STAMP(2);
     if (do_select) {
       // this wave's table entry and backup stores, visible to its own descent loads
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -194,6 +205,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
         status_sh = st;
         __hip_atomic_store(&sx.leaf_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      BK_OV_STAMP(3);
     }
   } else if (logits) {
     leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg);
@@ -201,12 +213,14 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     if (lane_id() == 0) done = __hip_atomic_fetch_add(&sx.done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     done = readlane_i(done, 0);
     if (done == kStepWaves - 2) {  // the last logit wave: every logit is in LDS
+      BK_OV_STAMP(4);
       while (__hip_atomic_load(&sx.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
         __builtin_amdgcn_s_sleep(1);
       const int err = readlane_i(sx.err, 0);
       if (err == 0) expand_children_lds(m, (int64_t)sx.off, K, ids, lg);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the children stored before the flag
       if (lane_id() == 0) __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      BK_OV_STAMP(5);
     }
   }
   if (do_select) {
@@ -217,8 +231,11 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     if (readlane_i(status_sh, 0) == 1) mask_slices_claim(dp, lsel, m32, &sx.slice);
   }
   __syncthreads();
+  if (wave == 0) BK_OV_STAMP(6);
   if (!do_select) return;
   select_leaf<kStepWaves, true>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
+  if (wave == 0) BK_OV_STAMP(7);
+#undef BK_OV_STAMP
 }
 
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
