@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3g(const float* __re
   const __amdgpu_buffer_rsrc_t wrs = ln_rsrc(wt, (unsigned)nlayers * kLayerBlocks * 1024u);
   // the tower: wave w = 2 mh + kh (below); its weights W[set][local chunk][m][part] (set = conv
   // parity) for output blocks 2mh + m and chunks 9kh + j; layer 0's in flight under the stem
-  const int kh = wave & 1, mh = wave >> 1;
+  const int kh = wave & 1;
   auto wload2 = [&](int layer, int c, int mb, int p) {
     return __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                          wrs, l * 16, ((layer * kLayerBlocks + c * 8 + mb * 2 + p) * 64) * 16, 0));

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   const int t = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #ifdef BK_STAMPS
-  // diag: 0 start, 1 prologue done, 2 wave 0 backup done, 3 wave 0 descent done, 4 the last logit
+  // diag: 0 start, 1 the new node's entry published (wave 1), 2 wave 0 backup done, 3 wave 0 descent done, 4 the last logit
   // wave done, 5 its children stored, 6 the next leaf's bitmask done (all waves), 7 end
 #define BK_OV_STAMP(i) \
   do { if (lane_id() == 0 && do_select && t < 4096) g_step_stamps[t][i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -178,27 +178,63 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     sx.done = 0;
     sx.leaf_ready = 0;
     sx.slice = 0;
+    sx.loaded = 0;
+    sx.counted = 0;
+    sx.written = 0;
+    sx.kready = 0;
+    sx.hready = 0;
     status_sh = 0;
   }
   if (wave == 0) BK_OV_STAMP(0);
   __syncthreads();
-  const int K = leaf_logits_prologue(dp, m, t, 0, feat, ldf, F, lds);
-  if (wave == 0) BK_OV_STAMP(1);
-  const bool logits = K >= 0 && K <= kLeafCap;  // block-uniform
+  // waves 1..: the logit prologue (legal ids compacted, features in LDS); wave 0 meanwhile backs
+  // the value up (independent of the logits) and then waits for K to publish the new node
+  int K = -1;
+  if (wave > 0) {
+    K = leaf_logits_prologue_w<kStepWaves - 1>(dp, m, t, feat, ldf, F, lds, wave, &sx);
+    if (wave == 1 && K >= 0) {
+      // the new node (table entry, child range) from wave 0's loads, as soon as K is known
+      wait_flag_acquire(&sx.hready);
+      StepHead h;
+      h.status = sx.hd_status;
+      h.node = sx.hd_node;
+      h.used = sx.hd_used;
+      h.key = sx.hd_key;
+      expand_head(m, t, h, K, &sx);
+      BK_OV_STAMP(1);
+    }
+  }
   const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
   float* lg = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap + F);
   uint32_t* lsel = lds + sel_off;
   uint32_t* m32 = lsel + kStateWords + 2 * kMaxN;
   if (wave == 0) {
-    expand_head_backup(m, t, dp.P, K, values, &sx);
+    const StepHead h = backup_first(m, t, dp.P, values);
+    if (h.status == 1) {
+      // wave 1 adds the new node once the leaf's ids are compacted
+      if (lane_id() == 0) {
+        sx.hd_status = h.status;
+        sx.hd_node = h.node;
+        sx.hd_used = h.used;
+        sx.hd_key = h.key;
+        __hip_atomic_store(&sx.hready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else if (lane_id() == 0) {
+      sx.err = -1;  // no new node: the children writer and the descent need not wait
+      __hip_atomic_store(&sx.ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     BK_OV_STAMP(2);
     if (do_select) {
-      // this wave's table entry and backup stores, visible to its own descent loads
+      // this wave's backup stores, visible to its own descent loads; the descent starts now and
+      // waits for the new node only if it reaches that board (pend: entry, children, failure)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       asm volatile("buffer_inv sc0" ::: "memory");
-      const int err = readlane_i(lane_id() == 0 ? sx.err : 0, 0);
-      const int64_t pend = (logits && err == 0) ? (int64_t)sx.off : -1;
-      const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lsel, pend, &sx.pready);
+      int* pend[3];
+      pend[0] = &sx.ready;
+      pend[1] = &sx.pready;
+      pend[2] = &sx.err;
+      const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lsel, h.key,
+                                    h.status == 1 ? pend : nullptr);
       if (st == 1)
         for (int i = lane_id(); i < dp.W32pad / 4; i += kWave) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
       if (lane_id() == 0) {
@@ -207,7 +243,8 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
       }
       BK_OV_STAMP(3);
     }
-  } else if (logits) {
+  }
+  if (wave > 0 && K >= 0 && K <= kLeafCap) {
     leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg);
     int done = 0;
     if (lane_id() == 0) done = __hip_atomic_fetch_add(&sx.done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);

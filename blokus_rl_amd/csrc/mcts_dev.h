@@ -208,9 +208,10 @@ __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K
 // terminal board, the path recorded (mcts.py:37-50); the leaf state stays in LDS for select_leaf.
 // lds = kStateWords + 2 kMaxN + W32pad words. Returns the leaf status (wave-uniform): 0 inactive
 // tree or error, 1 a leaf for the net, 2 a terminal board.
-// pend_off / pend_flag (k_leaf_step_ov): the children of the node at child offset pend_off are
-// still being written by another wave of the workgroup; the descent waits for pend_flag (set with
-// release semantics once they are stored) before it reads them.
+// pend_key / pend (k_leaf_step_ov): the node of board key pend_key is being added by other waves
+// of the workgroup (its table entry: flag pend[0]; then its children: pend[1]; pend[2] != 0 when
+// the entry was not made). Before the descent probes that key it waits for the entry, and before
+// it reads that node's children for them (flags set with release semantics).
 __device__ __forceinline__ void wait_flag_acquire(int* flag) {
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
   asm volatile("buffer_inv sc0" ::: "memory");
@@ -218,7 +219,7 @@ __device__ __forceinline__ void wait_flag_acquire(int* flag) {
 __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts& m, int t,
                                               const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
                                               double cpuct, int32_t* __restrict__ status_out, uint32_t* lds,
-                                              int64_t pend_off = -1, int* pend_flag = nullptr) {
+                                              uint64_t pend_key = 0, int* const* pend = nullptr) {
   uint32_t* s = lds;
   uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
   const int l = lane_id();
@@ -255,13 +256,17 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     int64_t off;
     int Kn;
     bool found;
-    BK_TACC(t_probe, found = table_find(m, t, table_key(s), off, Kn, nullptr));
+    const uint64_t key = table_key(s);
+    int* pend_children = nullptr;
+    if (pend && key == pend_key) {
+      wait_flag_acquire(pend[0]);  // the new node's table entry (or its failure) is published
+      if (readlane_i(*pend[2], 0) == 0) pend_children = pend[1];
+      pend = nullptr;
+    }
+    BK_TACC(t_probe, found = table_find(m, t, key, off, Kn, nullptr));
     if (!found) break;
     if (Kn <= 0) { err |= kErrIllegal; break; }  // a stored node always has a legal move
-    if (off == pend_off) {
-      wait_flag_acquire(pend_flag);
-      pend_off = -1;
-    }
+    if (pend_children) wait_flag_acquire(pend_children);  // and its children are stored
     scanned += Kn;
     int a, ci;
     BK_TACC(t_child, ci = select_child(m, off, Kn, cp, a));
@@ -706,66 +711,43 @@ struct StepExpand {
   int done;       // logit waves finished
   int leaf_ready; // wave 0's descent is done (status_sh, the leaf state and its zeroed mask in LDS)
   int slice;      // next leaf-bitmask slice to claim
+  int loaded;     // logit waves whose prologue loads are in LDS
+  int counted;    // logit waves whose word counts are in wcnt
+  int written;    // logit waves whose legal ids are in LDS
+  int kready;     // the leaf's legal ids are compacted: K + 1 (1 + -1 = 0 is never published)
+  int hready;     // wave 0 published hd (its backup is done)
+  int wcnt[16];   // legal ids per logit wave's 64-word segment of the leaf bitmask
+  int hd_status, hd_node;
+  long long hd_used;
+  unsigned long long hd_key;
 };
 
-// wave 0: expand_tree's loads (1), (2) without the children, the table entry, and the backup (3).
-// K = the prologue's leaf K. Publishes off / K / err (release) before the backup.
-__device__ __forceinline__ void expand_head_backup(const DevMcts& m, int t, int P, int K,
-                                                   const float* __restrict__ values, StepExpand* sx) {
+// wave 0, first: expand_tree's backup (3) with the loads it needs, plus the expansion's own loads
+// (node / child counters, leaf key) issued alongside — no dependence on the leaf's logits or K, so
+// it runs while the other waves stage and compact the leaf's legal ids. Returns the leaf status.
+struct StepHead {
+  int status, node;
+  int64_t used;
+  uint64_t key;
+};
+__device__ __forceinline__ StepHead backup_first(const DevMcts& m, int t, int P, const float* __restrict__ values) {
   __shared__ double vsh[kMaxP];
   const int l = lane_id();
-  const int status = m.leaf_status[t];
+  StepHead h;
+  h.status = m.leaf_status[t];
   const int depth = m.depth[t];
-  const int node = m.tree_nodes[t];
-  const int64_t used = m.tree_children[t];
-  const uint64_t key = table_key(m.leaf_state + (size_t)t * kStateWords);
-  if (status == 0) {
-    if (l == 0) {
-      sx->err = -1;
-      __hip_atomic_store(&sx->ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return;
-  }
+  h.node = m.tree_nodes[t];
+  h.used = m.tree_children[t];
+  h.key = table_key(m.leaf_state + (size_t)t * kStateWords);
+  if (h.status == 0) return h;
   const size_t pi = (size_t)t * kMaxDepth + l;
   const bool on_path = l < depth;  // depth <= kMaxDepth = 96: levels 64.. are handled below
   const int64_t pchild = on_path ? m.path_child[pi] : 0;
   const int ppl = on_path ? m.path_pl[pi] : 0;
-  int err = 0;
-  if (status == 1) {
-    const int64_t room = m.child_cap_per_tree - used;
-    if (K > kLeafCap) err |= kErrLeafCap;
-    if (node >= m.node_cap) err |= kErrTable;
-    if (K > room) err |= kErrChildPool;
-    int free_slot = -1;
-    if (!err) {
-      int64_t foff;
-      int fK;
-      if (table_find(m, t, key, foff, fK, &free_slot) || free_slot < 0) err |= kErrTable;
-    }
-    if (!err) {
-      if (l == 0) {
-        TabEntry e;
-        e.key = key;
-        e.off = (uint32_t)used;
-        e.K = K;
-        m.tab[(size_t)t * m.TS + free_slot] = e;
-        m.tree_nodes[t] = node + 1;
-        m.tree_children[t] = used + K;
-        ctr_add(m, t, kCtrExpanded, 1ull);
-        ctr_add(m, t, kCtrLeafK, (unsigned long long)K);
-      }
-    } else if (l == 0) {
-      atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
-    }
+  if (h.status == 1) {
     if (l < P) vsh[l] = (double)values[(size_t)t * P + l];
   } else {
     if (l < P) vsh[l] = m.leaf_scores[(size_t)t * kMaxP + l];
-  }
-  if (l == 0) {
-    sx->off = (long long)((int64_t)t * m.child_cap_per_tree + used);
-    sx->K = K;
-    sx->err = status == 1 ? err : -1;
-    __hip_atomic_store(&sx->ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   wave_lds_sync();
   if (on_path) {
@@ -784,6 +766,103 @@ __device__ __forceinline__ void expand_head_backup(const DevMcts& m, int t, int 
     m.ch_Q[ci] = ((double)n * q + v) / (double)(n + 1u);
     m.ch_N[ci] = n + 1u;
   }
+  return h;
+}
+
+// wave 0, then: the new node (expand_tree's checks, table slot and entry, counters) once K is
+// known; publishes off / K / err (release) for the wave that writes the children
+__device__ __forceinline__ void expand_head(const DevMcts& m, int t, const StepHead& h, int K, StepExpand* sx) {
+  const int l = lane_id();
+  int err = 0;
+  if (h.status == 1) {
+    const int64_t room = m.child_cap_per_tree - h.used;
+    if (K > kLeafCap) err |= kErrLeafCap;
+    if (h.node >= m.node_cap) err |= kErrTable;
+    if (K > room) err |= kErrChildPool;
+    int free_slot = -1;
+    if (!err) {
+      int64_t foff;
+      int fK;
+      if (table_find(m, t, h.key, foff, fK, &free_slot) || free_slot < 0) err |= kErrTable;
+    }
+    if (!err) {
+      if (l == 0) {
+        TabEntry e;
+        e.key = h.key;
+        e.off = (uint32_t)h.used;
+        e.K = K;
+        m.tab[(size_t)t * m.TS + free_slot] = e;
+        m.tree_nodes[t] = h.node + 1;
+        m.tree_children[t] = h.used + K;
+        ctr_add(m, t, kCtrExpanded, 1ull);
+        ctr_add(m, t, kCtrLeafK, (unsigned long long)K);
+      }
+    } else if (l == 0) {
+      atomicOr(&m.counters[kCtrErr], (unsigned long long)err);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the table entry stored before the flag
+  if (l == 0) {
+    sx->off = (long long)((int64_t)t * m.child_cap_per_tree + h.used);
+    sx->K = K;
+    sx->err = h.status == 1 ? err : -1;
+    __hip_atomic_store(&sx->ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// leaf_logits_prologue by the waves 1..NW of the workgroup only (wave 0 is backing up meanwhile):
+// their barriers are LDS counters; the compaction is parallel (each wave a 64-word segment of the
+// bitmask, offsets from the segment counts: the ids in ascending order, as compact_ids writes
+// them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32.
+template <int NW>
+__device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const DevMcts& m, int t,
+                                                      const float* __restrict__ feat, int64_t ldf, int F,
+                                                      uint32_t* lds, int wave, StepExpand* sx) {
+  uint32_t* m32 = lds;
+  int32_t* ids = reinterpret_cast<int32_t*>(lds + dp.W32pad);
+  float* f = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap);
+  if (m.leaf_status[t] != 1) return -1;  // uniform over these waves: no leaf to evaluate
+  const int tid = threadIdx.x - kWave, nth = NW * kWave, l = lane_id();
+  const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
+  for (int j = tid; j < dp.W64; j += nth) {
+    const uint64_t w = lm[j];
+    m32[2 * j] = (uint32_t)w;
+    m32[2 * j + 1] = (uint32_t)(w >> 32);
+  }
+  const float* ft = feat + (size_t)t * ldf;
+  for (int i = tid; i < F; i += nth) f[i] = ft[i];
+  auto arrive_wait = [&](int* ctr) {  // a barrier of the NW logit waves (LDS counter)
+    if (l == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NW) __builtin_amdgcn_s_sleep(1);
+  };
+  arrive_wait(&sx->loaded);
+  // this wave's segment: words 64 (wave - 1) .. + 63
+  const int w = 64 * (wave - 1) + l;
+  uint32_t bits = w < dp.W32 ? m32[w] : 0u;
+  const int cnt = __popc(bits);
+  const int incl = wave_incl_scan(cnt);
+  if (l == kWave - 1) sx->wcnt[wave] = incl;
+  arrive_wait(&sx->counted);
+  int before = 0, K = 0;
+  for (int v = 1; v <= NW; ++v) {
+    const int c = sx->wcnt[v];
+    before += v < wave ? c : 0;
+    K += c;
+  }
+  int pos = before + incl - cnt;
+  while (bits) {
+    const int b = __ffs(bits) - 1;
+    bits &= bits - 1u;
+    if (pos < kLeafCap) ids[pos] = w * 32 + b;
+    ++pos;
+  }
+  arrive_wait(&sx->written);
+  if (wave == 1 && l == 0) {
+    m.leaf_K[t] = K;
+    if (K > kLeafCap) atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrLeafCap);
+    __hip_atomic_store(&sx->kready, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  return K;
 }
 
 // The leaf bitmask of the state in LDS (s; m32 zeroed by the caller) built by whichever waves

@@ -30,7 +30,7 @@ a = buf[:256].astype(np.int64)
 ok = (a[:, 7] > 0) & (a[:, 4] > 0)
 a = a[ok]
 rel = a - a[:, :1]
-names = ["prologue", "wave0 backup", "wave0 descent", "logits (last wave)", "children", "mask done", "obs/end"]
+names = ["node added (wave 1)", "wave0 backup", "wave0 descent", "logits (last wave)", "children", "mask done", "obs/end"]
 out = {"trees": int(ok.sum()), "total_median": float(np.median(rel[:, 7])), "total_max": float(rel[:, 7].max()),
        "start_spread": float(a[:, 0].max() - a[:, 0].min())}
 for i, nm in zip([1, 2, 3, 4, 5, 6, 7], names):
