@@ -131,10 +131,14 @@ class BatchedMCTS:
         _check(self.lib.bk_mcts_simulate_const(self.h, _ptr(roots), _ptr(active), float(cpuct), int(nsims),
                                                _ptr(logp), _ptr(values), self._s()))
 
-    def root_policy(self, roots: torch.Tensor, active: torch.Tensor | None, temperature: float, cap: int = 2048):
-        ids = torch.zeros((self.T, cap), dtype=torch.int32, device=self.eng.device)
-        pi = torch.zeros((self.T, cap), dtype=torch.float64, device=self.eng.device)
-        counts = torch.zeros(self.T, dtype=torch.int32, device=self.eng.device)
+    def root_policy(self, roots: torch.Tensor, active: torch.Tensor | None, temperature: float, cap: int = 2048,
+                    zero: bool = True):
+        """ids/pi rows of every root (k_root); zero=False leaves the entries past each row's count
+        unwritten (bk_ply_policy reads only the first counts[t])."""
+        alloc = torch.zeros if zero else torch.empty
+        ids = alloc((self.T, cap), dtype=torch.int32, device=self.eng.device)
+        pi = alloc((self.T, cap), dtype=torch.float64, device=self.eng.device)
+        counts = alloc(self.T, dtype=torch.int32, device=self.eng.device)
         _check(self.lib.bk_mcts_root_policy(self.h, _ptr(roots), _ptr(active), float(temperature), _ptr(ids),
                                             _ptr(pi), cap, _ptr(counts), self._s()))
         return ids, pi, counts

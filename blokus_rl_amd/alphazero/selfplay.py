@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 
 import torch
 
-from ..engine import Engine
+from ..engine import Engine, _check, _ptr
 from .batched_mcts import BatchedMCTS
 
 
@@ -154,6 +154,8 @@ class SelfPlay:
         dev = eng.device
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(seed)
+        self._seed = int(seed) & 0xFFFFFFFFFFFFFFFF  # bk_ply_policy's counter-based draws
+        self._init_state = eng.init_states(1)  # bk_ply_finish restarts finished games from it
         self.roots = eng.init_states(games)
         self.active = torch.ones(games, dtype=torch.int32, device=dev)
         self.first_ply = torch.ones(games, dtype=torch.bool, device=dev)
@@ -352,6 +354,8 @@ class SelfPlay:
     # ------------------------------------------------------------------ one ply
     def play_ply(self, record: bool = True):
         self._simulations(self.num_sims)
+        if os.environ.get("BK_PLY_FUSED", "1") != "0":
+            return self._ply_tail_fused(record)
         ids, pi, counts = self.mcts.root_policy(self.roots, self.active, self.temperature, self.cap)
         G, cap = self.G, self.cap
         col = torch.arange(cap, device=self.eng.device).unsqueeze(0)
@@ -389,6 +393,51 @@ class SelfPlay:
         ended, scores = self.eng.game_ended(self.roots)
         done = ended.bool() & self.active.bool()
         self._finish(done, scores)
+        return status
+
+    def _ply_tail_fused(self, record: bool):
+        """The ply's tail (the tensor code of play_ply/_finish below, which BK_PLY_FUSED=0 keeps)
+        in four engine launches: k_root, bk_ply_policy (noise on first plies, float32 pi, the
+        sampled action, the record fields), k_next_state + k_game_ended, bk_ply_finish (z, counters,
+        restarts, next game ids), then the tree resets. The noise and the action come from
+        counter-based random numbers of (seed, ply, game) instead of self.gen: the same law
+        (tests/test_selfplay_gpu.py::test_play_ply_sampling_statistics), ~0.45 ms less per ply."""
+        eng, G, cap, dev = self.eng, self.G, self.cap, self.eng.device
+        lib = self.mcts.lib
+        ids, pi, counts = self.mcts.root_policy(self.roots, self.active, self.temperature, cap, zero=False)
+        action = torch.empty(G, dtype=torch.int32, device=dev)
+        ids16 = torch.empty((G, cap), dtype=torch.int16, device=dev)
+        pi32 = torch.empty((G, cap), dtype=torch.float32, device=dev)
+        act = torch.empty(G, dtype=torch.bool, device=dev)
+        player = torch.empty(G, dtype=torch.int32, device=dev)
+        st = self.mcts._s()
+        _check(lib.bk_ply_policy(_ptr(ids), _ptr(pi), _ptr(counts), _ptr(self.active), _ptr(self.first_ply), G, cap,
+                                 float(self.weight), float(self.alpha), self._seed, self._stats.plies,
+                                 _ptr(self.roots), _ptr(action), _ptr(ids16), _ptr(pi32), _ptr(act), _ptr(player),
+                                 st))
+        if record:
+            # nothing here is written in place later (the next roots and game ids are new tensors)
+            rec = (self.roots, ids16, pi32, counts, player, self.game_id, act)
+            self._records.append(rec)
+            self._window.append(rec)
+            if self.record_plies and len(self._records) > self.record_plies:
+                self._dropped_plies += len(self._records) - self.record_plies
+                del self._records[:-self.record_plies]
+                del self._window[:-self.record_plies]
+        nxt, _, status = eng.next_state(self.roots, action)
+        ended, scores = eng.game_ended(nxt)
+        self._stats.plies += 1
+        self._ensure_zcap()
+        roots_out = eng.empty_states(G)
+        gid_out = torch.empty_like(self.game_id)
+        flags = torch.empty(G, dtype=torch.int32, device=dev)
+        _check(lib.bk_ply_finish(G, eng.P, _ptr(ended), _ptr(scores), _ptr(counts), _ptr(act), _ptr(self.game_id),
+                                 _ptr(nxt), _ptr(self._init_state), int(self.continuous), int(self.num_sims),
+                                 _ptr(self.active), _ptr(self.first_ply), _ptr(flags), _ptr(gid_out), _ptr(roots_out),
+                                 _ptr(self.z_table), _ptr(self.z_known), self._zcap, _ptr(self._next_gid),
+                                 _ptr(self._fin_dev), _ptr(self._sims_dev), _ptr(self._cap_overflow), st))
+        self.mcts.reset(flags)  # a new MCTS per episode (trainer.py:95); no-op for unflagged trees
+        self.roots, self.game_id = roots_out, gid_out
         return status
 
     def _finish(self, done: torch.Tensor, scores: torch.Tensor):

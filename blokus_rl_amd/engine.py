@@ -55,6 +55,10 @@ _SIGS = {
     "bk_mcts_root_stats": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "bk_mcts_counters": (_i, [_vp, _vp, _vp]),
     "bk_mcts_leaf_info": (_i, [_vp, _vp, _vp, _vp]),
+    "bk_ply_policy": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, ctypes.c_double, ctypes.c_double, ctypes.c_uint64,
+                           ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bk_ply_finish": (_i, [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                           ctypes.c_int64, _vp, _vp, _vp, _vp, _vp]),
     "bk_vec_reset": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "bk_vec_step": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "bk_replay_stride": (ctypes.c_size_t, [_i]),

@@ -215,6 +215,31 @@ int bk_mcts_leaf_info(bk_mcts* m, void* leaf_states, int32_t* depths, void* stre
  * (sum of K over descended nodes), out[7] children created by expansion. */
 int bk_mcts_counters(bk_mcts* m, int64_t* out, void* stream);
 
+/* The self-play ply's tail after the search, per game g < G (trainer.py:108-137; one launch each
+ * instead of the per-op tensor code). bk_ply_policy: from bk_mcts_root_policy's ids/pi/counts
+ * rows (`cap` wide), on a game's first ply (first_ply[g] != 0) pi = (1 - w) pi + w Dir(alpha) over
+ * its counts[g] legal ids (trainer.py:110-116, float64), pi32 = float32(pi) (trainer.py:124), the
+ * action = ids[g][i] with i drawn from pi32 (np.random.choice, trainer.py:125) or -1 when the game
+ * is inactive or has no legal id (counts <= 0); record fields ids16 (int16 ids, 0 past K), pi32
+ * (0 past K), act_mask (1 = the game moved), player (the mover). Random numbers are counter-based
+ * in (seed, ply, g): one call per ply with a new `ply` value. 0 < cap <= 4096.
+ * bk_ply_finish (one workgroup): games with active && ended store z_table[game_id] = scores
+ * (float32, trainer.py:134-135) and z_known = 1, get reset_flags = 1 (for bk_mcts_reset: a new
+ * tree per episode, trainer.py:95) and count into fin_count; continuous != 0 restarts them from
+ * init_state (one state) with ids *next_gid + (finished games before g), advancing *next_gid;
+ * otherwise active[g] = 0. first_ply = (first_ply && !act_mask) || restarted; sims_count +=
+ * num_sims x (games that moved); cap_overflow = 1 if an active game had counts < 0. roots_out
+ * (a different buffer than roots) receives the next roots, game_id_out the next ids. */
+int bk_ply_policy(const int32_t* ids, const double* pi, const int32_t* counts, const int32_t* active,
+                  const uint8_t* first_ply, int G, int cap, double dirichlet_weight, double dirichlet_alpha,
+                  uint64_t seed, uint64_t ply, const void* roots, int32_t* action, int16_t* ids16, float* pi32,
+                  uint8_t* act_mask, int32_t* player, void* stream);
+int bk_ply_finish(int G, int P, const int32_t* ended, const double* scores, const int32_t* counts,
+                  const uint8_t* act_mask, const int64_t* game_id, const void* roots, const void* init_state,
+                  int continuous, int num_sims, int32_t* active, uint8_t* first_ply, int32_t* reset_flags,
+                  int64_t* game_id_out, void* roots_out, float* z_table, uint8_t* z_known, int64_t zcap,
+                  int64_t* next_gid, int64_t* fin_count, int64_t* sims_count, int32_t* cap_overflow, void* stream);
+
 /* ---------------------------------------------------------------- config 5: PPO vector env
  * The blokus_gym `blokus-simple-v0` env as the PPO trainer drives it (ppo/trainer.py:128-175,
  * :380-386): 2-player preset, the agent is colour 0 against a built-in uniform-random opponent

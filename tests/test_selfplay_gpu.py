@@ -188,3 +188,47 @@ def test_play_ply_sampling_statistics():
         assert o.game_ended(fin[g]).tolist() == z[g].tolist(), g
     ex = sp.examples()
     assert set(map(tuple, ex.z.cpu().numpy().tolist())) <= set(map(tuple, z.tolist()))
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_fused_ply_tail_matches_tensor_tail(monkeypatch, continuous):
+    """bk_ply_policy + bk_ply_finish (the default ply tail) against play_ply's tensor code
+    (BK_PLY_FUSED=0) where the draws do not matter: temperature 0 and no noise weight make pi
+    one-hot, so both tails take the same actions and must leave identical records, roots, game
+    ids, flags, z table and counters over whole games (7x7, 2 players; continuous mode restarts
+    finished games with the next ids)."""
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import DumbNet
+
+    eng = Engine(7, 2, 5)
+    torch.manual_seed(0)
+    net = DumbNet(7, 2, eng.A).to(eng.device).eval()
+    runs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("BK_PLY_FUSED", fused)
+        sp = SelfPlay(eng, net, 48, num_sims=6, seed=5, temperature=0.0, dirichlet_weight=0.0,
+                      continuous=continuous, cap=256)
+        for _ in range(40):
+            sp.play_ply()
+        sp.check()
+        runs.append(sp)
+    a, b = runs
+    assert a.stats.games_finished == b.stats.games_finished > 0
+    assert a.stats.sims == b.stats.sims
+    for x, y in ((a.roots, b.roots), (a.game_id, b.game_id), (a.active, b.active), (a.first_ply, b.first_ply),
+                 (a.z_table[: b.z_table.shape[0]], b.z_table[: a.z_table.shape[0]]),
+                 (a.z_known[: b.z_known.shape[0]], b.z_known[: a.z_known.shape[0]]), (a._next_gid, b._next_gid)):
+        assert torch.equal(x, y)
+    assert len(a._records) == len(b._records)
+    for ra, rb in zip(a._records, b._records):
+        m = ra[6]
+        assert torch.equal(m, rb[6])
+        for i in (0, 3, 4, 5):
+            assert torch.equal(ra[i], rb[i]), i
+        k = ra[3].clamp(min=0)
+        col = torch.arange(ra[1].shape[1], device=eng.device).unsqueeze(0)
+        valid = col < k.unsqueeze(1)
+        assert torch.equal(torch.where(valid, ra[1], 0), torch.where(valid, rb[1], 0))
+        assert torch.equal(torch.where(valid, ra[2], 0), torch.where(valid, rb[2], 0))
+        assert bool((ra[2][~valid] == 0).all()) and bool((ra[1][~valid] == 0).all())

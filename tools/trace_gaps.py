@@ -34,3 +34,14 @@ span = win[-1][1] - win[0][0]
 out = {"window_us": span / 1e3, "kernel_busy_frac": busy / span,
        "gap_us_median": {f"{k[0]}->{k[1]}": [round(float(np.median(v)), 2), len(v)] for k, v in gaps.items() if len(v) >= 3}}
 print(json.dumps(out, indent=1))
+# where the window's time goes: per kernel class (busy us) and the idle time between kernels
+cls = collections.defaultdict(float)
+cnt = collections.Counter()
+for s, e, k in win:
+    cls[k] += (e - s) / 1e3
+    cnt[k] += 1
+idle = sum((b[0] - a[1]) / 1e3 for a, b in zip(win, win[1:]) if b[0] > a[1])
+plies = max(1, cnt["k_root"])
+print(json.dumps({"plies_in_window": plies, "busy_us_per_ply": {k: round(v / plies, 1) for k, v in cls.items()},
+                  "launches_per_ply": {k: round(v / plies, 1) for k, v in cnt.items()},
+                  "idle_us_per_ply": round(idle / plies, 1)}, indent=1))
