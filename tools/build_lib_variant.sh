@@ -10,7 +10,7 @@ mkdir -p "$obj" blokus_rl_amd/_lib/exp
 rm -f "$obj"/*.o
 cd "$src"
 pids=()
-for f in env.hip mcts.hip vecenv.hip train.hip ppo.hip netops.hip conv.hip sims.hip leafnet.hip leafnet_wino.hip leafnet_g.hip; do
+for f in env.hip mcts.hip vecenv.hip train.hip ppo.hip netops.hip conv.hip sims.hip leafnet.hip leafnet_wino.hip leafnet_g.hip ply.hip; do
   [ -f "$f" ] || continue
   XF=""; [ "$f" = conv.hip ] || [ "$f" = sims.hip ] && XF="-fno-slp-vectorize"
   [ "$f" = leafnet_wino.hip ] && XF="-fno-slp-vectorize -ffp-contract=fast"

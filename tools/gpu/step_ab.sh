@@ -1,15 +1,8 @@
 #!/bin/bash
-# GPU session: new/changed tests, the wx3 A/B timing, and self-play with and without the
-# overlapped leaf step. Stops at the first step that ends in anything but pass/fail (fault,
-# abort, timeout).
+# leaf-step change: the search parity tests on the in-tree build, then self-play sims/s of the
+# in-tree build vs blokus_rl_amd/_lib/exp/libprev.so (tools/gpu/lib_ab.sh, 3 rounds)
 cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out
-ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
-TESTS=${TESTS:-"tests/test_sims_gpu.py tests/test_search_parity_gpu.py tests/test_dropin_gpu.py tests/test_selfplay_gpu.py"} bash tools/gpu/newtests.sh
-rc=$?; ok $rc || exit $rc
-timeout -k 10 120 python tools/wx3_bench.py > gpurun_out/wxb.log 2>&1
-rc=$?; tail -3 gpurun_out/wxb.log; ok $rc || exit $rc
-timeout -k 10 200 python bench.py --workload selfplay --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/sp_ov.json 2> gpurun_out/sp_ov.err
-rc=$?; cut -c1-300 gpurun_out/sp_ov.json; [ $rc -eq 0 ] || exit $rc
-BK_STEP_OVERLAP=0 timeout -k 10 200 python bench.py --workload selfplay --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/sp_noov.json 2> gpurun_out/sp_noov.err
-rc=$?; cut -c1-300 gpurun_out/sp_noov.json; exit $rc
+mkdir -p gpurun_out/step
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_sims_gpu.py tests/test_search_parity_gpu.py tests/test_mcts_gpu.py > gpurun_out/step/pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/step/pytest.log; [ $rc -eq 0 ] || exit $rc
+ROUNDS=3 bash tools/gpu/lib_ab.sh "" blokus_rl_amd/_lib/exp/libprev.so
