@@ -327,17 +327,27 @@ __global__ __launch_bounds__(64) void k_root(DevMcts m, const uint32_t* __restri
   // N^(1/T), summed left to right like Python's object-array sum, then normalised.
   // N^1 is exact in the reference (int ** 1.0); device pow() is not correctly rounded, so the
   // default temperature 1 bypasses it. Other temperatures agree to ~1 ulp with host libm.
+  // The terms are computed by all lanes into LDS, lane 0 adds them in index order from there (a
+  // chain of adds fed by pipelined LDS reads, not a global-memory round trip per term: the
+  // sequential loop over the output row took 65-155 us per launch mid-game at K ~ 300-700), and
+  // the divisions run on all lanes again: the same terms, order and quotients.
+  constexpr int kRootLds = 2048;
+  __shared__ double vals[kRootLds];
+  __shared__ double total_sh;
   const double e = 1.0 / temperature;
-  for (int i = l; i < Kc; i += kWave) o[i] = raise_visits(m.ch_N[off + i], e);
+  for (int i = l; i < K && i < kRootLds; i += kWave) vals[i] = raise_visits(m.ch_N[off + i], e);
   __syncthreads();
   if (l == 0) {
     double total = 0.0;
-    for (int i = 0; i < K; ++i) total += (i < Kc) ? o[i] : raise_visits(m.ch_N[off + i], e);
-    if (total == 0.0) {
-      for (int i = 0; i < Kc; ++i) o[i] = 1.0 / (double)K;
-    } else {
-      for (int i = 0; i < Kc; ++i) o[i] = o[i] / total;
-    }
+#pragma unroll 8
+    for (int i = 0; i < K; ++i) total += i < kRootLds ? vals[i] : raise_visits(m.ch_N[off + i], e);
+    total_sh = total;
+  }
+  __syncthreads();
+  const double total = total_sh;
+  for (int i = l; i < Kc; i += kWave) {
+    const double v = i < kRootLds ? vals[i] : raise_visits(m.ch_N[off + i], e);
+    o[i] = total == 0.0 ? 1.0 / (double)K : v / total;
   }
 }
 
