@@ -397,9 +397,9 @@ class SelfPlay:
 
     def _ply_tail_fused(self, record: bool):
         """The ply's tail (the tensor code of play_ply/_finish below, which BK_PLY_FUSED=0 keeps)
-        in four engine launches: k_root, bk_ply_policy (noise on first plies, float32 pi, the
-        sampled action, the record fields), k_next_state + k_game_ended, bk_ply_finish (z, counters,
-        restarts, next game ids), then the tree resets. The noise and the action come from
+        in six engine launches: k_root, bk_ply_policy (noise on first plies, float32 pi, the
+        sampled action, the record fields), k_next_state, k_game_ended, bk_ply_finish (z, counters,
+        restarts, next game ids), then the tree resets (k_reset). The noise and the action come from
         counter-based random numbers of (seed, ply, game) instead of self.gen: the same law
         (tests/test_selfplay_gpu.py::test_play_ply_sampling_statistics), ~0.45 ms less per ply."""
         eng, G, cap, dev = self.eng, self.G, self.cap, self.eng.device
