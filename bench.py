@@ -649,6 +649,9 @@ def main():
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
+        if "k_leaf_step" in out.get("search_roofline", {}).get("kernel", ""):
+            # HBM-side bytes per launch of the search kernel (profiles/r03_pmc_leafstep.json)
+            out["search_roofline"]["traffic"] = _pmc_traffic("k_leaf_step_ov", args.games)
         kname = out["roofline"].get("kernel", "").split(" ")[0]
         if kname.startswith("k_conv3x3") or kname.startswith("k_tower") or kname.startswith("k_leafnet"):
             # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)
