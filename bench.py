@@ -25,6 +25,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from blokus_rl_amd.replay import dist_active  # noqa: E402
+
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
 
 # Algorithmic bytes of one board in k_legal_mask: the packed state read (384 B) + the
@@ -67,9 +69,18 @@ def dist_backend() -> str:
 
 
 def _dist_init(need_gpu: bool = True):
+    """One process per GPU (torchrun's RANK / LOCAL_RANK / WORLD_SIZE). A process group is made at
+    world size > 1, and at world size 1 when BK_DIST_BACKEND is set (e.g. nccl: the multi-GPU
+    path's collectives — the all-gather inside the timed region, max-over-ranks timing, DDP — run
+    through RCCL on a one-GPU box)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and os.environ.get("BK_DIST_BACKEND"):
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     if need_gpu:
         ndev = torch.cuda.device_count()
         if ndev == 0:
@@ -77,7 +88,7 @@ def _dist_init(need_gpu: bool = True):
                                "--workload dry rehearses the launch on CPU)")
         dev = local % ndev  # one rank per GPU; a gloo rehearsal may put several ranks on one
         torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or os.environ.get("BK_DIST_BACKEND"):
         backend = dist_backend() if need_gpu else "gloo"
         kw = {"device_id": torch.device("cuda", torch.cuda.current_device())} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
@@ -85,7 +96,7 @@ def _dist_init(need_gpu: bool = True):
 
 
 def _barrier(world):
-    if world > 1:
+    if dist_active():
         dist.barrier()
 
 
@@ -94,7 +105,7 @@ def _coll_device():
 
 
 def _max_over_ranks(x: float, world: int) -> float:
-    if world == 1:
+    if not dist_active():
         return x
     t = torch.tensor([x], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -102,7 +113,7 @@ def _max_over_ranks(x: float, world: int) -> float:
 
 
 def _sum_over_ranks(x: float, world: int) -> float:
-    if world == 1:
+    if not dist_active():
         return x
     t = torch.tensor([float(x)], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t)
@@ -125,7 +136,7 @@ def bench_dry(args, world, rank):
     buf, cap = rp.pack(states, ids, pi, k, z)
     _barrier(world)
     t0 = time.perf_counter()
-    if world > 1:
+    if dist_active():
         rows, cap = rp.all_gather_packed(buf, cap)
     else:
         rows = buf
@@ -137,7 +148,7 @@ def bench_dry(args, world, rank):
             "unit": "rows", "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": dt * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": "dry", "parallelism": f"dp{world}"}, "ranks_seen": seen,
-            "backend": dist.get_backend() if world > 1 else None}
+            "backend": dist.get_backend() if dist_active() else None}
 
 
 def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
@@ -593,8 +604,8 @@ def bench_ppo(args, world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=25)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train", "ppo", "dry"],
                     default="all")
     ap.add_argument("--ppo-updates", type=int, default=2)
@@ -632,7 +643,7 @@ def main():
         out = bench_dry(args, world, rank)
         if rank == 0:
             print(json.dumps(out), flush=True)
-        if world > 1:
+        if dist_active():
             dist.destroy_process_group()
         return
     if world != args.gpus and rank == 0:
@@ -649,9 +660,15 @@ def main():
     else:
         from blokus_rl_amd.alphazero.selfplay_bench import bench_selfplay, run_selfplay
         out = bench_selfplay(args, world, rank)
-        if "k_leaf_step" in out.get("search_roofline", {}).get("kernel", ""):
-            # HBM-side bytes per launch of the search kernel (profiles/r03_pmc_leafstep.json)
-            out["search_roofline"]["traffic"] = _pmc_traffic("k_leaf_step_ov", args.games)
+        sr = out.get("search_roofline", {})
+        if "k_leaf_step" in sr.get("kernel", ""):
+            # HBM-side bytes per launch of the search kernel (profiles/*pmc*leafstep*.json) over its
+            # live launch time: the fraction of the HBM roofline it actually draws
+            tr = _pmc_traffic("k_leaf_step_ov", args.games)
+            sr["traffic"] = tr
+            if tr and sr.get("k_leaf_step_us"):
+                sr["achieved"] = tr / (sr["k_leaf_step_us"] * 1e-6) / 1e9
+                sr["frac"] = sr["achieved"] / sr["peak"]
         kname = out["roofline"].get("kernel", "").split(" ")[0]
         if kname.startswith("k_conv3x3") or kname.startswith("k_tower") or kname.startswith("k_leafnet"):
             # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)
@@ -699,9 +716,11 @@ def main():
     if args.cpu_pool is not None:
         args.cpu_pool.close()
         args.cpu_pool.join()
+    if dist_active():
+        out["dist_backend"] = dist.get_backend()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_active():
         dist.destroy_process_group()
 
 

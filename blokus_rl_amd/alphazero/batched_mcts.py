@@ -34,7 +34,6 @@ class BatchedMCTS:
         self.status = torch.zeros(trees, dtype=torch.int32, device=dev)
         self.obs = torch.zeros((trees,) + eng.obs_shape, dtype=torch.float32, device=dev)
         self.leaf_mask = torch.zeros((trees, eng.W), dtype=torch.int64, device=dev)
-        self._sim_cache = None  # simulate_resnet: (model, parameter views, scratch, ctypes args)
 
     def __del__(self):
         try:
@@ -50,10 +49,15 @@ class BatchedMCTS:
     def reset(self, flags: torch.Tensor | None = None):
         _check(self.lib.bk_mcts_reset(self.h, _ptr(flags), self._s()))
 
-    def select(self, roots: torch.Tensor, active: torch.Tensor | None, cpuct: float = 1.0):
-        """Descend every active tree to a leaf; returns (status[T], obs[T,2P,N,N], mask[T,W])."""
-        _check(self.lib.bk_mcts_select(self.h, _ptr(roots), _ptr(active), float(cpuct), _ptr(self.status),
-                                       _ptr(self.obs), _ptr(self.leaf_mask), self._s()))
+    def select(self, roots: torch.Tensor, active: torch.Tensor | None, cpuct: float = 1.0, root_eps: float = 1e-6):
+        """Descend every active tree to a leaf; returns (status[T], obs[T,2P,N,N], mask[T,W]).
+        root_eps: the root's term under the square root of mcts.py:43 (1e-6 = epsilon_fix, 0 = not)."""
+        if root_eps == 1e-6:
+            _check(self.lib.bk_mcts_select(self.h, _ptr(roots), _ptr(active), float(cpuct), _ptr(self.status),
+                                           _ptr(self.obs), _ptr(self.leaf_mask), self._s()))
+        else:
+            _check(self.lib.bk_mcts_select_eps(self.h, _ptr(roots), _ptr(active), float(cpuct), float(root_eps),
+                                               _ptr(self.status), _ptr(self.obs), _ptr(self.leaf_mask), self._s()))
         return self.status, self.obs, self.leaf_mask
 
     def expand_backup(self, logp: torch.Tensor | None, values: torch.Tensor, prior_mode: int = 0):
@@ -87,49 +91,6 @@ class BatchedMCTS:
                                           _ptr(self.obs) if sel else None, _ptr(self.leaf_mask) if sel else None,
                                           self._s()))
         return (self.status, self.obs, self.leaf_mask) if sel else None
-
-    @staticmethod
-    def fused_resnet_ok(eng: Engine, model) -> bool:
-        """simulate_resnet's net: a HIP nets.LeafResNet with the 8-plane stem (4 players), at least one
-        residual block and a board size the fused tower supports (14, 20); k_sims runs the f32
-        tower, so only when the staged path runs it too (BK_NET_MATH=f32)."""
-        from ..nets import LeafResNet, net_math, tower_enabled
-
-        return (net_math() == "f32" and isinstance(model, LeafResNet) and model.native and model.f.stem.in_channels == 8
-                and len(model.f.blocks) > 0 and tower_enabled() and bool(eng.lib.bk_tower_supported(eng.N)))
-
-    def simulate_resnet(self, roots: torch.Tensor, active: torch.Tensor | None, cpuct: float, nsims: int, model):
-        """`nsims` simulations of every active tree in ONE launch (bk_mcts_simulate_resnet, k_sims): a
-        workgroup per tree runs select -> the leaf ResNet (stem, Winograd tower, heads) -> the policy
-        Linear over the leaf's legal ids -> expand/backup, nsims times, with no grid-wide step between
-        the stages. The same trees, bitwise, as nsims rounds of select(), model(obs) (features=True),
-        leaf_logits() and expand_backup(mode 2). model: see fused_resnet_ok()."""
-        _check(self.lib.bk_mcts_simulate_resnet(self.h, _ptr(roots), _ptr(active), float(cpuct), int(nsims),
-                                                *self._sim_args(model), self._s()))
-
-    def _sim_args(self, model):
-        if self._sim_cache is None or self._sim_cache[0] is not model:
-            f, N, P, T = model.f, self.eng.N, self.eng.P, self.T
-            c = lambda x: x.detach().float().contiguous()  # noqa: E731
-            params = [model.w_stem_tower, c(f.stem.bias), model.u_tower, model.b_tower,
-                      c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias), c(f.value_conv.weight.view(64)),
-                      c(f.value_conv.bias), f.value_fc1_wt(), c(f.value_fc1.bias), c(f.value_fc2.weight),
-                      c(f.value_fc2.bias), c(f.policy_out.weight), c(f.policy_out.bias)]
-            e = lambda n: torch.empty((T, n), dtype=torch.float32, device=self.eng.device)  # noqa: E731
-            scratch = [e(2 * P * N * N), e(N * N * 64), e(N * N * 64), e(N * N * 64), e(2 * N * N), e(P)]
-            args = [2 * len(f.blocks)] + [_ptr(x) for x in params + scratch]
-            self._sim_cache = (model, params, scratch, args)
-        return self._sim_cache[3]
-
-    def simulate_const(self, roots: torch.Tensor, active: torch.Tensor | None, cpuct: float, nsims: int,
-                       logp: torch.Tensor, values: torch.Tensor):
-        """`nsims` simulations of every active tree in ONE launch (bk_mcts_simulate_const) with a leaf
-        evaluation that does not depend on the leaf (DumbNet: logp [T, A] and values [T, P] for every
-        leaf of tree t): the trees of nsims rounds of select() + expand_backup(logp, values, 0)."""
-        assert logp.dtype == torch.float32 and logp.shape == (self.T, self.eng.A)
-        assert values.dtype == torch.float32 and values.shape == (self.T, self.eng.P)
-        _check(self.lib.bk_mcts_simulate_const(self.h, _ptr(roots), _ptr(active), float(cpuct), int(nsims),
-                                               _ptr(logp), _ptr(values), self._s()))
 
     def root_policy(self, roots: torch.Tensor, active: torch.Tensor | None, temperature: float, cap: int = 2048,
                     zero: bool = True):

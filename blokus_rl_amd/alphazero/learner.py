@@ -123,10 +123,11 @@ class Learner:
         self.batch_size = batch_size
         self.policy_fn = policy_fn
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        up = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if up else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
         self.net = model
-        if self.world > 1:
+        if up:  # DDP whenever a group is up (at world size 1 too: the RCCL path on a one-GPU box)
             dev = next(model.parameters()).device
             self.net = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[dev.index] if dev.type == "cuda" else None, process_group=group)

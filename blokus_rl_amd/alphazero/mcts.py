@@ -53,10 +53,10 @@ class MCTS:
         return {"nodes": self._m.counters()["nodes"]}
 
     def simulate(self, s, current_player: int, cpuct: float = 1, epsilon_fix: bool = True):
-        if not epsilon_fix:
-            raise NotImplementedError("the engine always uses sqrt(sum N + 1e-6) (epsilon_fix=True)")
+        # epsilon_fix: sqrt(N.sum() + 1e-6) at the root, else sqrt(N.sum() + 0) (mcts.py:43); deeper
+        # levels always take 1e-6 (the recursive call of mcts.py:50 passes the default)
         roots = self.game._dev(s)
-        status, obs, mask = self._m.select(roots, None, float(cpuct))
+        status, obs, mask = self._m.select(roots, None, float(cpuct), 1e-6 if epsilon_fix else 0.0)
         st = int(status[0])
         if st == 2:
             leaves, _ = self._m.leaf_info()

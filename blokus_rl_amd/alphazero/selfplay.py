@@ -171,10 +171,7 @@ class SelfPlay:
         self._ensure_zcap()
         self._records: list[tuple[torch.Tensor, ...]] = []  # per-ply records (z resolved lazily)
         self.timers = None
-        self._fused_ok: bool | None = None
         self._graph = None  # the captured simulations (_sim_graph)
-        # fused path: simulations per launch (0: all of a ply's in one launch)
-        self.sims_per_launch = int(os.environ.get("BK_SIMS_PER_LAUNCH", "0"))
         self._window: list[tuple[torch.Tensor, ...]] = []  # records since mark_window()
         self._dropped_plies = 0  # continuous mode: plies that fell out of the record ring
         # an active game whose root had more children than `cap` (k_root returns counts = -K):
@@ -251,30 +248,9 @@ class SelfPlay:
         d = max(k for k in range(1, 101) if num_sims % k == 0)
         return d if d >= 10 else 10
 
-    def fused(self) -> bool:
-        """Whole simulations in one launch (k_sims: the HIP ResNet in fp32 with the sparse policy
-        head; k_sims_const: DumbNet) when BK_SIM_FUSED=1 and no stage timers are on. Off by default:
-        bitwise the same trees, but measured slower than the per-stage launches replayed from a HIP
-        graph (round 1: 508k vs 557k sims/s at config 3)."""
-        if self._fused_ok is None:
-            ev = self.evaluator
-            self._fused_ok = ev.model is None or bool(
-                ev.sparse and ev.dtype == torch.float32 and BatchedMCTS.fused_resnet_ok(self.eng, ev.model))
-        return self._fused_ok and self.timers is None and os.environ.get("BK_SIM_FUSED", "0") == "1"
-
     def _simulations(self, n: int):
-        """n simulations of every active tree: fused launches (fused()), else replays of a graph of
-        sim_graph_sims captured simulations (no per-launch host work) and eager ones."""
-        if self.fused():
-            ev = self.evaluator
-            k = self.sims_per_launch if self.sims_per_launch > 0 else max(n, 1)
-            for s in range(0, n, k):
-                c = min(k, n - s)
-                if ev.model is None:
-                    self.mcts.simulate_const(self.roots, self.active, self.cpuct, c, ev.const_logp, ev.const_v)
-                else:
-                    self.mcts.simulate_resnet(self.roots, self.active, self.cpuct, c, ev.model)
-            return
+        """n simulations of every active tree: replays of a graph of sim_graph_sims captured
+        simulations (no per-launch host work) and eager ones."""
         k = self.sim_graph_sims
         if n >= k and self._graph_usable():
             g = self._sim_graph()

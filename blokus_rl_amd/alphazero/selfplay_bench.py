@@ -12,8 +12,10 @@ import time
 import torch
 import torch.distributed as dist
 
+
 from ..engine import Engine
 from ..nets import build_model
+from ..replay import dist_active
 from .selfplay import SelfPlay
 
 FP32_PEAK = 157.3e12             # MI355X_MICROARCH.md (f32 vector = f32 MFMA)
@@ -94,7 +96,7 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     for _ in range(warmup):
         sp.play_ply()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_active():
         dist.barrier()
     torch.cuda.synchronize()
     c0 = sp.mcts.counters()
@@ -104,7 +106,7 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     t0 = time.perf_counter()
     for _ in range(steps):
         sp.play_ply()
-    if world > 1:
+    if dist_active():
         # config 4: the (s, pi, z) rows of the timed plies, all-gathered over RCCL/xGMI
         from ..replay import all_gather_packed
 
@@ -115,7 +117,7 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
         gather = {"rows_sent": int(buf.shape[0]), "rows_received": int(rows.shape[0]),
                   "bytes_received": int(rows.numel()), "seconds": time.perf_counter() - tg}
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_active():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -129,30 +131,9 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
 
 
 def stage_times(sp) -> dict:
-    """Stage times outside the timed region. Fused path: a ply's simulations timed with HIP events
-    on their stream ('k_sims' / 'k_sims_const': ms, launches, leaves expanded and, for the ResNet,
-    the MFMA FLOP of their leaf nets). Then one ply launched stage by stage with events around each
-    stage: select / net / expand ms per sim-step."""
+    """Stage times outside the timed region: one ply launched stage by stage with events around
+    each stage: select / net / expand ms per sim-step."""
     out = {}
-    if sp.fused():
-        st = torch.cuda.current_stream(sp.eng.device)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        c0 = sp.mcts.counters()
-        e0.record(st)
-        sp._simulations(sp.num_sims)
-        e1.record(st)
-        torch.cuda.synchronize()
-        leaves = sp.mcts.counters()["expanded"] - c0["expanded"]
-        k = sp.sims_per_launch if sp.sims_per_launch > 0 else sp.num_sims
-        rec = {"ms": e0.elapsed_time(e1), "sims": sp.num_sims, "launches": -(-sp.num_sims // k), "leaves": leaves}
-        model = sp.evaluator.model
-        if model is not None:
-            N, convs = sp.eng.N, 2 * len(model.f.blocks)
-            per_leaf = 2.0 * 16 * 64 * 64 * (N // 2) ** 2 * convs + 2.0 * N * N * 64 * 9 * model.f.stem.in_channels
-            rec.update(convs=convs, flop_per_leaf=per_leaf, flop=per_leaf * leaves)
-            out["k_sims"] = rec
-        else:
-            out["k_sims_const"] = rec
     sp.enable_timers(True)
     sp.play_ply()
     out.update(sp.timer_ms())
@@ -252,7 +233,7 @@ def bench_selfplay(args, world, rank):
     sp, eng, sims, elapsed, delta, ms = run_selfplay(args.model, args.nn_dtype, G, args.sims, args.steps,
                                                      args.warmup, rank, args.node_cap, world)
     local_sims = sims
-    if world > 1:
+    if dist_active():
         t = torch.tensor([elapsed, float(sims)], dtype=torch.float64, device="cuda")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -264,15 +245,21 @@ def bench_selfplay(args, world, rank):
     ls = time_leaf_step(sp)
     if ls is not None:
         # the search launches of the timed path (k_select + k_leaf_step), timed live
-        search = {"bound": "hbm", "kernel": "k_select (once per ply) + k_leaf_step (per simulation: sparse policy "
-                                            "head, expand/backup, next descent + leaf bitmask/observation)",
-                  "achieved": ls["bytes_per_sim_step"] / (ls["ms_per_sim_step"] * 1e-3) / 1e9,
-                  "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                  "frac": ls["bytes_per_sim_step"] / (ls["ms_per_sim_step"] * 1e-3) / HBM_PEAK, "traffic": None,
-                  "bytes_per_sim_step": ls["bytes_per_sim_step"], "search_ms_per_sim_step": ls["ms_per_sim_step"],
-                  "k_leaf_step_us": ls["k_leaf_step_us"],
-                  "note": "bytes as the kernels move them; the policy-Linear rows (97 MB table) are counted per "
-                          "use and served mostly from the 256 MB Infinity Cache"}
+        # not an HBM-bound kernel: a chain of dependent L2/MALL round trips (the descent) beside a
+        # gather that L2 mostly serves (PMC: about a third of the addressed bytes leave L2). So the
+        # line carries the bytes as the kernels address them (policy-Linear rows counted per use)
+        # as `addressed_*`, and the HBM fraction only from the measured HBM-side bytes per launch
+        # (`traffic`, attached by bench.py from the committed PMC passes) over the live launch time
+        addressed = ls["bytes_per_sim_step"] / (ls["ms_per_sim_step"] * 1e-3)
+        search = {"bound": "latency/L2", "kernel": "k_leaf_step_ov (per simulation: sparse policy head, "
+                                                   "expand/backup, next descent + leaf bitmask/observation; "
+                                                   "k_select once per ply)",
+                  "achieved": None, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": None, "traffic": None,
+                  "addressed_bytes_per_sim_step": ls["bytes_per_sim_step"], "addressed_GBps": addressed / 1e9,
+                  "search_ms_per_sim_step": ls["ms_per_sim_step"], "k_leaf_step_us": ls["k_leaf_step_us"],
+                  "note": "achieved/frac = HBM-side bytes per k_leaf_step_ov launch (rocprofv3 PMC, "
+                          "FETCH_SIZE x2 + WRITE_SIZE, profiles/*pmc*leafstep*.json) / the live launch time; "
+                          "addressed_* count the bytes as the kernels address them (each W row per use)"}
     else:
         sbytes = search_bytes(delta, local_sims, obs_bytes, 8 * eng.W)
         search_ms = ms.get("select", 0.0) + ms.get("expand", 0.0)

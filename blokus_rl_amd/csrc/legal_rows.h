@@ -31,9 +31,6 @@ struct RowCtx {
 // forbidden and anchor accumulators), then legal = anchor & ~forbidden, validity masks, and the
 // W-bit field ORed into the board's LDS bitmask (two 32-bit ORs; the second is 0 unless the field
 // straddles a word).
-#ifdef BK_NOATOMIC  // timing experiment only (wrong masks): plain stores instead of LDS atomics
-#define atomicOr(p, v) (*(p) = (v))
-#endif
 #ifndef BK_MASK_SPLIT
 #define BK_MASK_SPLIT 0  // A/B knob: even / odd origin rows in separate LDS atomics (leaf bitmask)
 #endif

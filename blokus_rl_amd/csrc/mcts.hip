@@ -53,12 +53,12 @@ constexpr int kSelectWaves = 4;
 __global__ __launch_bounds__(64 * kSelectWaves) void k_select(DevPreset dp, DevMcts m, const uint32_t* __restrict__ roots,
                                                               const int32_t* __restrict__ active, double cpuct,
                                                               int32_t* __restrict__ status_out, float* __restrict__ obs,
-                                                              uint64_t* __restrict__ mask_out) {
+                                                              uint64_t* __restrict__ mask_out, double root_eps) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ int status_sh;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wave == 0) {
-    const int st = select_descend(dp, m, blockIdx.x, roots, active, cpuct, status_out, lds);
+    const int st = select_descend(dp, m, blockIdx.x, roots, active, cpuct, status_out, lds, 0, nullptr, root_eps);
     if (lane_id() == 0) status_sh = st;
   }
   __syncthreads();
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
                                                                     float* __restrict__ obs,
                                                                     uint64_t* __restrict__ mask_out, int sel_off) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ int status_sh;
+  __shared__ int status_sh, status0_sh;
   __shared__ StepExpand sx;
   const int t = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -184,14 +184,18 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     sx.kready = 0;
     sx.hready = 0;
     status_sh = 0;
+    // the leaf status this step expands, read once before the barrier: wave 0's next descent
+    // rewrites m.leaf_status[t] while the logit waves may still be deciding whether to run
+    status0_sh = m.leaf_status[t];
   }
   if (wave == 0) BK_OV_STAMP(0);
   __syncthreads();
+  const int status0 = status0_sh;
   // waves 1..: the logit prologue (legal ids compacted, features in LDS); wave 0 meanwhile backs
   // the value up (independent of the logits) and then waits for K to publish the new node
   int K = -1;
   if (wave > 0) {
-    K = leaf_logits_prologue_w<kStepWaves - 1>(dp, m, t, feat, ldf, F, lds, wave, &sx);
+    K = leaf_logits_prologue_w<kStepWaves - 1>(dp, m, t, feat, ldf, F, lds, wave, &sx, status0);
     if (wave == 1 && K >= 0) {
       // the new node (table entry, child range) from wave 0's loads, as soon as K is known
       wait_flag_acquire(&sx.hready);
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   uint32_t* lsel = lds + sel_off;
   uint32_t* m32 = lsel + kStateWords + 2 * kMaxN;
   if (wave == 0) {
-    const StepHead h = backup_first(m, t, dp.P, values);
+    const StepHead h = backup_first(m, t, dp.P, values, status0);
     if (h.status == 1) {
       // wave 1 adds the new node once the leaf's ids are compacted
       if (lane_id() == 0) {
@@ -456,14 +460,20 @@ int bk_mcts_reset(bk_mcts* m, const int32_t* reset_flags, void* stream) {
   return launch_check("k_reset");
 }
 
-int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int32_t* leaf_status,
-                   float* obs, uint64_t* leaf_mask, void* stream) {
+int bk_mcts_select_eps(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, double root_eps,
+                       int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream) {
   BK_REQUIRE(m && roots && leaf_status && obs, "bad argument");
+  BK_REQUIRE(root_eps >= 0.0, "bk_mcts_select_eps: root_eps >= 0");
   const DevPreset& dp = m->ctx->dp;
   const size_t lds = sizeof(uint32_t) * (size_t)(kStateWords + 2 * kMaxN + dp.W32pad);
   hipLaunchKernelGGL(k_select, dim3(m->d.T), dim3(kWave * kSelectWaves), lds, (hipStream_t)stream, dp, m->d,
-                     (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask);
+                     (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, root_eps);
   return launch_check("k_select");
+}
+
+int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int32_t* leaf_status,
+                   float* obs, uint64_t* leaf_mask, void* stream) {
+  return bk_mcts_select_eps(m, roots, active, cpuct, 1e-6, leaf_status, obs, leaf_mask, stream);
 }
 
 int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,

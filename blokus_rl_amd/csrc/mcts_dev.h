@@ -151,7 +151,9 @@ constexpr int kSelB = 12;
 #ifndef BK_MASK_WPB
 #define BK_MASK_WPB 16  // A/B knob: waves that take orientations in a leaf bitmask (the rest idle)
 #endif
-__device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, double cp, int& id_out) {
+// eps: the term under the square root (mcts.py:43: 1e-6 with epsilon_fix, the default, else 0)
+__device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, double cp, int& id_out,
+                                            double eps = 1e-6) {
   const int l = lane_id();
   double best = -INFINITY;
   int bi = 0x7fffffff, bid = 0;
@@ -181,7 +183,7 @@ __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K
     uint32_t vs = 0u;
 #pragma unroll
     for (int u = 0; u < kSelB; ++u) vs += l + u * kWave < K ? nn[u] : 0u;
-    const double sq = sqrt((double)(uint32_t)wave_sum((int)vs) + 1e-6);
+    const double sq = sqrt((double)(uint32_t)wave_sum((int)vs) + eps);
 #pragma unroll
     for (int u = 0; u < kSelB; ++u) {
       const int i = l + u * kWave;
@@ -193,7 +195,7 @@ __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K
   } else {  // two passes: the visit sum, then the scan
     uint32_t vs = 0u;
     for (int i = l; i < K; i += kWave) vs += Nn[i];
-    const double sq = sqrt((double)(uint32_t)wave_sum((int)vs) + 1e-6);
+    const double sq = sqrt((double)(uint32_t)wave_sum((int)vs) + eps);
     for (int i = l; i < K; i += kWave) {
       const double h = Q[i] + ((cp * (double)P[i]) * sq) / (1.0 + (double)Nn[i]);
       if (h > best) { best = h; bi = i; bid = ID[i]; }
@@ -219,7 +221,8 @@ __device__ __forceinline__ void wait_flag_acquire(int* flag) {
 __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts& m, int t,
                                               const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
                                               double cpuct, int32_t* __restrict__ status_out, uint32_t* lds,
-                                              uint64_t pend_key = 0, int* const* pend = nullptr) {
+                                              uint64_t pend_key = 0, int* const* pend = nullptr,
+                                              double root_eps = 1e-6) {
   uint32_t* s = lds;
   uint64_t* fa = reinterpret_cast<uint64_t*>(lds + kStateWords);
   const int l = lane_id();
@@ -235,7 +238,7 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
   load_state(s, roots + (size_t)t * kStateWords);
   BK_BOARD_SYNC();
   BK_STAMP(0, 1);
-  double cp = cpuct;
+  double cp = cpuct, eps = root_eps;
   int depth = 0, err = 0;
   long long scanned = 0;
 #ifdef BK_STAMPS
@@ -269,7 +272,7 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     if (pend_children) wait_flag_acquire(pend_children);  // and its children are stored
     scanned += Kn;
     int a, ci;
-    BK_TACC(t_child, ci = select_child(m, off, Kn, cp, a));
+    BK_TACC(t_child, ci = select_child(m, off, Kn, cp, a, eps));
     // no child won the argmax: every PUCT score was NaN (a NaN prior or value from a diverged
     // net); flag it and stop before the unchecked placement and the path record
     if (ci < 0 || ci >= Kn) { err |= kErrIllegal; break; }
@@ -286,7 +289,8 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
       m.path_pl[pi] = (int)s[kWToMove];
     }
     ++depth;
-    cp = 1.0;  // the recursive call of mcts.py:50 passes no cpuct
+    cp = 1.0;    // the recursive call of mcts.py:50 passes no cpuct
+    eps = 1e-6;  // nor epsilon_fix (its default True)
   }
   BK_STAMP(0, 2);
 #ifdef BK_STAMPS
@@ -730,11 +734,14 @@ struct StepHead {
   int64_t used;
   uint64_t key;
 };
-__device__ __forceinline__ StepHead backup_first(const DevMcts& m, int t, int P, const float* __restrict__ values) {
+// status: the tree's leaf status as the step found it (read once, before any wave of the step can
+// run the next descent, which rewrites leaf_status)
+__device__ __forceinline__ StepHead backup_first(const DevMcts& m, int t, int P, const float* __restrict__ values,
+                                                 int status) {
   __shared__ double vsh[kMaxP];
   const int l = lane_id();
   StepHead h;
-  h.status = m.leaf_status[t];
+  h.status = status;
   const int depth = m.depth[t];
   h.node = m.tree_nodes[t];
   h.used = m.tree_children[t];
@@ -813,15 +820,16 @@ __device__ __forceinline__ void expand_head(const DevMcts& m, int t, const StepH
 // leaf_logits_prologue by the waves 1..NW of the workgroup only (wave 0 is backing up meanwhile):
 // their barriers are LDS counters; the compaction is parallel (each wave a 64-word segment of the
 // bitmask, offsets from the segment counts: the ids in ascending order, as compact_ids writes
-// them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32.
+// them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32. status: the leaf status
+// the step started from (not m.leaf_status, which wave 0's next descent rewrites meanwhile).
 template <int NW>
 __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const DevMcts& m, int t,
                                                       const float* __restrict__ feat, int64_t ldf, int F,
-                                                      uint32_t* lds, int wave, StepExpand* sx) {
+                                                      uint32_t* lds, int wave, StepExpand* sx, int status) {
   uint32_t* m32 = lds;
   int32_t* ids = reinterpret_cast<int32_t*>(lds + dp.W32pad);
   float* f = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap);
-  if (m.leaf_status[t] != 1) return -1;  // uniform over these waves: no leaf to evaluate
+  if (status != 1) return -1;  // uniform over these waves: no leaf to evaluate
   const int tid = threadIdx.x - kWave, nth = NW * kWave, l = lane_id();
   const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
   for (int j = tid; j < dp.W64; j += nth) {

@@ -35,8 +35,9 @@ __device__ __forceinline__ double u01(uint64_t x) { return ((double)(x >> 11) + 
 
 // Gamma(alpha, 1): alpha = 1 -> -log(u); else Marsaglia-Tsang (alpha < 1 boosted by u^(1/alpha)),
 // normals by Box-Muller; at most 32 rounds (the acceptance rate is > 95% per round for alpha >= 1)
+constexpr int kGammaSlots = 128;  // draw slots per entry: the boost + 3 per round x 32 rounds = 97 <= 128
 __device__ double gamma_draw(double alpha, uint64_t seed, uint64_t ply, int game, int idx) {
-  int k = idx * 72;  // 72 draw slots per entry
+  int k = idx * kGammaSlots;
   if (alpha == 1.0) return -log(u01(ply_rng(seed, ply, game, k)));
   double boost = 1.0, a = alpha;
   if (a < 1.0) {
@@ -146,19 +147,27 @@ __global__ __launch_bounds__(kPlyThreads) void k_ply_policy(const int32_t* __res
   const double target = (1.0 - u01(ply_rng(seed, ply, g, 0x7fffffff))) * total;  // [0, total)
   const double base = scan[tid];
   if (hi > lo && target >= base && target < base + cs) {
+    // the chunk claims the target: its first entry whose running sum passes it, or — when the walk
+    // (base + p0 + p1 + ...) rounds below the chunk test's base + cs — its last positive entry
     double acc = base;
+    int last = -1, at = -1;
     for (int i = lo; i < hi; ++i) {
       acc += (double)p32[i];
-      if (p32[i] > 0.0f && acc > target) {
-        atomicMax(&pick, i);  // one chunk holds the target (a rounding tie at most delays it)
-        break;
+      if (p32[i] > 0.0f) {
+        last = i;
+        if (acc > target) {
+          at = i;
+          break;
+        }
       }
     }
+    if (at < 0) at = last;
+    if (at >= 0) atomicMax(&pick, at);
   }
   __syncthreads();
   if (tid == 0) {
     int i = pick;
-    if (i < 0) {  // rounding at the very end: the last positive entry
+    if (i < 0) {  // no chunk claimed the target (rounding at the very end): the last positive entry
       for (i = K - 1; i > 0 && !(p32[i] > 0.0f); --i) {
       }
     }

@@ -45,12 +45,11 @@ _SIGS = {
     "bk_mcts_destroy": (_i, [_vp]),
     "bk_mcts_reset": (_i, [_vp, _vp, _vp]),
     "bk_mcts_select": (_i, [_vp, _vp, _vp, ctypes.c_double, _vp, _vp, _vp, _vp]),
+    "bk_mcts_select_eps": (_i, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp, _vp]),
     "bk_mcts_expand_backup": (_i, [_vp, _vp, _vp, _i, _vp]),
     "bk_mcts_leaf_logits": (_i, [_vp, _vp, ctypes.c_int64, _i, _vp, _vp, _vp]),
     "bk_mcts_leaf_step": (_i, [_vp, _vp, ctypes.c_int64, _i, _vp, _vp, _vp, _i, _vp, _vp, ctypes.c_double, _vp,
                                _vp, _vp, _vp]),
-    "bk_mcts_simulate_resnet": (_i, [_vp, _vp, _vp, ctypes.c_double, _i, _i] + [_vp] * 21),
-    "bk_mcts_simulate_const": (_i, [_vp, _vp, _vp, ctypes.c_double, _i, _vp, _vp, _vp]),
     "bk_mcts_root_policy": (_i, [_vp, _vp, _vp, ctypes.c_double, _vp, _vp, _i, _vp, _vp]),
     "bk_mcts_root_stats": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "bk_mcts_counters": (_i, [_vp, _vp, _vp]),
@@ -84,13 +83,6 @@ _SIGS = {
     "bk_leafnet_x3_weight_bytes": (_i, [_i]),
     "bk_leafnet_x3_supported": (_i, [_i]),
     "bk_leafnet_x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8 + [_i, _vp, _vp, _vp, _vp]),
-    "bk_leafnet_wx3_weight_bytes": (_i, []),
-    "bk_leafnet_wx3_supported": (_i, [_i]),
-    "bk_leafnet_wx3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8
-                       + [_i, _vp, _vp, _vp, _vp, _vp]),
-    "bk_leafnet_x3g_supported": (_i, [_i]),
-    "bk_leafnet_x3g": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8
-                       + [_i, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

@@ -298,46 +298,6 @@ def pack_x3(w: torch.Tensor, b: torch.Tensor | None = None) -> tuple[torch.Tenso
     return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous(), bound.to(w.device)
 
 
-def wx3_channel(ks: int, ch: int, e: int) -> int:
-    """bk_leafnet_wx3's K order: element e of k-group ks in K chunk ch is input channel
-    4 * slot + e % 4 with slot = 8 (ks & 1) + 4 (ks >> 1) + 2 ch + e // 4 (leafnet_wino.hip
-    wx_slot: the bank-conflict-free grid slots of the window reads)."""
-    return 4 * (8 * (ks & 1) + 4 * (ks >> 1) + 2 * ch + e // 4) + e % 4
-
-
-def pack_wx3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-    """[64, 64, 3, 3] tower conv weights -> bk_leafnet_wx3's operands: (the Winograd F(2x2,3x3) U =
-    G w G^T, computed in fp64, scaled per output channel by 2^e_o so that its largest magnitude
-    over (channel, position) lies in [2^14, 2^15) and split hi = f16(x), lo = f16(x - hi), as
-    uint8 bytes; inverse scales 2^-e_o f32 [64]). Fragment order [xi1 4][m 4][xi2 4][chunk 2]
-    [part hi/lo][lane 64][8 f16]: wave xi1, lane l = 16 ks + r holds U[16 m + r][wx3_channel(ks,
-    chunk, e)] at (xi1, xi2), e = 0..7 — the A operand of v_mfma_f32_16x16x32_f16 for output
-    block m."""
-    assert w.shape == (64, 64, 3, 3)
-    G = torch.tensor(_WINO_G, dtype=torch.float64)
-    U = torch.einsum("ik,ockl,jl->ocij", G, w.detach().to("cpu", torch.float64), G)  # [o][c][xi1][xi2]
-    mx = U.abs().amax(dim=(1, 2, 3))
-    _, e = torch.frexp(mx)
-    e = torch.where(mx > 0, 15 - e, torch.zeros_like(e)).to(torch.float64)
-    scaled = U * torch.pow(2.0, e).view(64, 1, 1, 1)
-    hi = scaled.to(torch.float16)
-    lo = (scaled - hi.to(torch.float64)).to(torch.float16)
-    parts = torch.stack([hi, lo])                                 # [part][o][c][xi1][xi2]
-    chan = torch.tensor([[[wx3_channel(ks, ch, el) for el in range(8)] for ks in range(4)] for ch in range(2)])
-    q = torch.arange(4).view(4, 1, 1, 1, 1, 1, 1, 1)
-    m = torch.arange(4).view(1, 4, 1, 1, 1, 1, 1, 1)
-    x = torch.arange(4).view(1, 1, 4, 1, 1, 1, 1, 1)
-    ch = torch.arange(2).view(1, 1, 1, 2, 1, 1, 1, 1)
-    pt = torch.arange(2).view(1, 1, 1, 1, 2, 1, 1, 1)
-    ks = torch.arange(4).view(1, 1, 1, 1, 1, 4, 1, 1)
-    r = torch.arange(16).view(1, 1, 1, 1, 1, 1, 16, 1)
-    el = torch.arange(8).view(1, 1, 1, 1, 1, 1, 1, 8)
-    c = chan[ch, ks, el]                                          # broadcast to the full index shape
-    packed = parts[pt, 16 * m + r, c, q, x].contiguous()          # [q][m][xi2][ch][part][ks][r][8]
-    inv = torch.pow(2.0, -e).to(torch.float32)
-    return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous()
-
-
 def net_math() -> str:
     """The leaf ResNet's arithmetic on the device: "x3" (default) = bk_leafnet_x3, split-f16 MFMA
     products with f32 accumulation (fp32-class accuracy, tests/test_leafnet_gpu.py); "f32" =
@@ -345,8 +305,8 @@ def net_math() -> str:
     import os
 
     m = os.environ.get("BK_NET_MATH", "x3")
-    if m not in ("x3g", "wx3", "x3", "f32"):
-        raise ValueError(f"BK_NET_MATH must be x3g, wx3, x3 or f32, got {m!r}")
+    if m not in ("x3", "f32"):
+        raise ValueError(f"BK_NET_MATH must be x3 or f32, got {m!r}")
     return m
 
 
@@ -373,60 +333,6 @@ def leafnet_x3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
         _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), _ptr(model.x3_bounds),
         *[_ptr(t) for t in h[1:]], P, _ptr(pf),
         _ptr(v), None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
-    return (pf, v, out) if want_out else (pf, v)
-
-
-def leafnet_wx3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
-    """bk_leafnet_wx3: as leafnet_x3 with the residual tower as Winograd F(2x2,3x3) convolutions on
-    split-f16 MFMA products (20x20 boards)."""
-    from .engine import _check, _ptr, _stream, load_library
-
-    B, cin, N, _ = obs.shape
-    assert cin == 8 and obs.dtype == torch.float32 and obs.is_contiguous()
-    f = model.f
-    lib = load_library()
-    nl = 2 * len(f.blocks)
-    assert model.wx3_utower.numel() == nl * lib.bk_leafnet_wx3_weight_bytes()
-    assert model.x3_wstem.numel() == lib.bk_leafnet_x3_weight_bytes(8)
-    P = f.value_fc2.out_features
-    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=obs.device)
-    v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
-    x0 = torch.empty((B, N * N, 64), dtype=torch.float32, device=obs.device)
-    out = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device,
-                      memory_format=torch.channels_last) if want_out else None
-    h = model.x3_heads
-    _check(lib.bk_leafnet_wx3(
-        ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
-        _ptr(model.wx3_utower), _ptr(model.wx3_sutower), _ptr(model.b_tower), _ptr(model.x3_bounds),
-        *[_ptr(t) for t in h[1:]], P, _ptr(pf), _ptr(v), _ptr(x0),
-        None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
-    return (pf, v, out) if want_out else (pf, v)
-
-
-def leafnet_x3g(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
-    """bk_leafnet_x3g: leafnet_x3's net with the tower convolutions group-major (20x20 boards): the
-    tower output bitwise leafnet_x3's, the heads summed in another order."""
-    from .engine import _check, _ptr, _stream, load_library
-
-    B, cin, N, _ = obs.shape
-    assert cin == 8 and obs.dtype == torch.float32 and obs.is_contiguous()
-    f = model.f
-    lib = load_library()
-    nl = 2 * len(f.blocks)
-    assert model.x3_wtower.numel() == nl * lib.bk_leafnet_x3_weight_bytes(64)
-    assert model.x3_wstem.numel() == lib.bk_leafnet_x3_weight_bytes(8)
-    P = f.value_fc2.out_features
-    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=obs.device)
-    v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
-    x0 = torch.empty((B, N * N, 64), dtype=torch.float32, device=obs.device)
-    out = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device,
-                      memory_format=torch.channels_last) if want_out else None
-    h = model.x3_heads
-    _check(lib.bk_leafnet_x3g(
-        ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
-        _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), _ptr(model.x3_bounds),
-        *[_ptr(t) for t in h[1:]], P, _ptr(pf), _ptr(v), _ptr(x0),
-        None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
     return (pf, v, out) if want_out else (pf, v)
 
 
@@ -566,11 +472,6 @@ class LeafResNet(nn.Module):
                 self.register_buffer("x3_wtower", torch.cat([p[0] for p in packs]).contiguous())
                 self.register_buffer("x3_stower", torch.cat([p[1] for p in packs]).contiguous())
                 self.register_buffer("x3_bounds", torch.cat([bs] + [p[2] for p in packs]).contiguous())
-                if f.stem.out_channels == 64 and all(c.weight.shape == (64, 64, 3, 3) for c in convs):
-                    # bk_leafnet_wx3's tower operands (Winograd U, split)
-                    wp = [pack_wx3(c.weight) for c in convs]
-                    self.register_buffer("wx3_utower", torch.cat([p[0] for p in wp]).contiguous())
-                    self.register_buffer("wx3_sutower", torch.cat([p[1] for p in wp]).contiguous())
                 c = lambda t: t.detach().float().contiguous().clone()  # noqa: E731
                 heads = [c(f.stem.bias), c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias),
                          c(f.value_conv.weight.view(64)), c(f.value_conv.bias), c(f.value_fc1_wt()),
@@ -594,21 +495,7 @@ class LeafResNet(nn.Module):
             from .engine import load_library
 
             math = net_math() if self.x3 else "f32"
-            if math == "x3g" and load_library().bk_leafnet_x3g_supported(x.shape[2]):
-                # the whole net in one launch, the tower convs group-major (bk_leafnet_x3g)
-                pf, v = leafnet_x3g(x.float().contiguous(), self)
-                if self.features:
-                    return pf, v
-                logits = f.policy_out(pf)
-                return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
-            if math == "wx3" and load_library().bk_leafnet_wx3_supported(x.shape[2]):
-                # the whole net in one launch, the tower as Winograd convs on split-f16 products
-                pf, v = leafnet_wx3(x.float().contiguous(), self)
-                if self.features:
-                    return pf, v
-                logits = f.policy_out(pf)
-                return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
-            if math in ("x3", "wx3", "x3g") and load_library().bk_leafnet_x3_supported(x.shape[2]):
+            if math == "x3" and load_library().bk_leafnet_x3_supported(x.shape[2]):
                 # the whole net in one launch on split-f16 MFMA products (bk_leafnet_x3)
                 pf, v = leafnet_x3(x.float().contiguous(), self)
                 if self.features:

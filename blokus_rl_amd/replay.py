@@ -15,6 +15,12 @@ STATE = 384
 HEADER = STATE + 4 + 4 + 16
 
 
+def dist_active() -> bool:
+    """A process group is up (also at world size 1: `BK_DIST_BACKEND=nccl python bench.py --gpus 1`
+    runs the collectives of the multi-GPU path on one device)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def stride_of(cap: int) -> int:
     s = HEADER + cap * 2 + cap * 4
     return (s + 15) // 16 * 16

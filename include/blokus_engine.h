@@ -140,6 +140,12 @@ int bk_mcts_reset(bk_mcts* m, const int32_t* reset_flags, void* stream);
  *   leaf_mask: [T][mask_words] legal bits of the leaf (status 1), for the masked softmax. */
 int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double cpuct,
                    int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream);
+/* The same with the root's exploration term under the square root given: mcts.py:43 adds
+ * (1e-6 if epsilon_fix else 0) to N.sum() at the root only (the recursive call of mcts.py:50
+ * passes the default epsilon_fix=True, so every deeper level uses 1e-6). root_eps = 1e-6 is
+ * bk_mcts_select; MCTS.simulate(..., epsilon_fix=False) passes 0. */
+int bk_mcts_select_eps(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, double root_eps,
+                       int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream);
 
 /* Expansion + backup (mcts.py:50-56 and :63-70): for status-1 leaves create the node with
  * P = exp(log_softmax(logp[t][legal ids])) (neural_network.py:159-173) and back up
@@ -171,29 +177,6 @@ int bk_mcts_leaf_logits(bk_mcts* m, const float* feat, int64_t ldf, int F, const
 int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const float* W, const float* bias,
                       const float* values, int do_select, const void* roots, const int32_t* active, double cpuct,
                       int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream);
-
-/* Whole simulations in one launch (sims.hip, k_sims): for every active tree, nsims x { select ->
- * the leaf ResNet (stem, Winograd residual tower, heads) -> the policy Linear over the leaf's
- * legal ids -> expand/backup (mode 2) }, one workgroup per tree, no grid-wide step between the
- * stages; the trees of nsims rounds of bk_mcts_select, bk_resnet_stem_tower_heads,
- * bk_mcts_leaf_logits and bk_mcts_expand_backup(mode 2), bitwise. Replaces the simulation loop
- * `for _ in range(num_mcts_sims): tree.simulate(...)` (trainer.py:104-105, mcts_player.py:16-17;
- * MCTS.simulate, mcts.py:13-71, with predict, neural_network.py:92-110, at each leaf). 14x14 or
- * 20x20 boards, 4 players; nlayers and the weights as for bk_resnet_stem_tower_heads, policy_w
- * [A][2NN] and policy_b [A] (policy_out, models/blokus_nnet.py:147); f32 scratch, 16-byte
- * aligned: obs [T][8][N][N], x0 / hA / hB [T][N][N][64], pf [T][2NN], v [T][P]. */
-int bk_mcts_simulate_resnet(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int nsims,
-                            int nlayers, const float* wstem, const float* bstem, const float* u2all,
-                            const float* biasall, const float* wp, const float* bp, const float* wv,
-                            const float* bv, const float* w1t, const float* b1, const float* w2, const float* b2,
-                            const float* policy_w, const float* policy_b, float* obs, float* x0, float* hA,
-                            float* hB, float* pf, float* v, void* stream);
-
-/* The same with a leaf evaluation that does not depend on the leaf (DumbNet, compare_arena.py:87-95:
- * logp [T][A] and values [T][P] for every leaf of tree t), k_sims_const, one wave per tree: the
- * trees of nsims rounds of bk_mcts_select + bk_mcts_expand_backup(logp, values, 0). */
-int bk_mcts_simulate_const(bk_mcts* m, const void* roots, const int32_t* active, double cpuct, int nsims,
-                           const float* logp, const float* values, void* stream);
 
 /* get_distribution (mcts.py:73-99) at the root of every active tree: ids[t][0..K) and
  * pi[t][0..K) (f64) in child order, K in counts[t]; temperature 0 -> one-hot argmax N
@@ -364,37 +347,6 @@ int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, co
                   int nlayers, const void* wtower, const float* stower, const float* btower, const float* bounds,
                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
                   const float* w2, const float* b2, int P, float* pf, float* vout, float* out, void* stream);
-
-/* The same leaf ResNet with the residual tower as Winograd F(2x2,3x3) convolutions on split-f16
- * MFMA products (leafnet_wino.hip): 2.25x fewer matrix products, same fp32-class accuracy. The
- * stem, heads and arguments as bk_leafnet_x3 except the tower: utower = nlayers x
- * bk_leafnet_wx3_weight_bytes() bytes of split U = G g G^T in the kernel's fragment order
- * (nets.py pack_wx3), sutower [nlayers][64] its inverse scales; x0ws [B][N*N][64] f32 device
- * workspace (the stem output kept for the tower's final residual). N = 20
- * (bk_leafnet_wx3_supported). Replaces the same reference forward as bk_leafnet_x3
- * (models/blokus_nnet.py:135-150 via neural_network.py:92-110). */
-int bk_leafnet_wx3_weight_bytes(void);
-int bk_leafnet_wx3_supported(int N);
-int bk_leafnet_wx3(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
-                   int nlayers, const void* utower, const float* sutower, const float* btower, const float* bounds,
-                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t,
-                   const float* b1, const float* w2, const float* b2, int P, float* pf, float* vout, float* x0ws,
-                   float* out, void* stream);
-
-/* The same leaf ResNet as bk_leafnet_x3 (same operands: pack_x3 weights, scales, bounds, heads)
- * with the residual tower's convolutions group-major (leafnet_g.hip): each wave keeps its output
- * channels' weights for a whole conv in registers and runs the 25 pixel groups one after another,
- * the epilogue of group g-1 and the delayed grid writes of group g-4 under group g's MFMAs, so no
- * layer ends in an epilogue with the matrix cores idle. The tower output is bitwise bk_leafnet_x3's;
- * the heads sum in another order (fp32 rounding). x0ws: device workspace of B x N*N x 64 floats
- * (the stem output for the final residual). N = 20 (bk_leafnet_x3g_supported). Replaces the same
- * reference forward (models/blokus_nnet.py:135-150 via neural_network.py:92-110). */
-int bk_leafnet_x3g_supported(int N);
-int bk_leafnet_x3g(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
-                   int nlayers, const void* wtower, const float* stower, const float* btower, const float* bounds,
-                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t,
-                   const float* b1, const float* w2, const float* b2, int P, float* pf, float* vout, float* x0ws,
-                   float* out, void* stream);
 
 #ifdef __cplusplus
 }

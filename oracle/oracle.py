@@ -194,13 +194,13 @@ class MCTSOracle:
         self.tree: dict[int, dict] = {}
         self.terminal_hits = 0
 
-    def simulate(self, s: np.ndarray, cpuct: float = 1.0):
+    def simulate(self, s: np.ndarray, cpuct: float = 1.0, epsilon_fix: bool = True):
         h = self.o.hash(s)
         player = Oracle.to_move(s)
         if h in self.tree:  # mcts.py:39-57
             node = self.tree[h]
             N, Q, P = node["N"], node["Q"], node["P"]
-            sq = math.sqrt(float(sum(N)) + 1e-6)
+            sq = math.sqrt(float(sum(N)) + (1e-6 if epsilon_fix else 0))  # mcts.py:43
             best, best_i = -math.inf, 0
             for i in range(len(N)):
                 u = cpuct * P[i] * sq / (1 + N[i])
@@ -208,7 +208,7 @@ class MCTSOracle:
                 if hv > best:
                     best, best_i = hv, i
             s2, p2 = self.o.next_state(s, node["ids"][best_i])
-            scores = self.simulate(s2)  # cpuct not forwarded (mcts.py:50)
+            scores = self.simulate(s2)  # cpuct, epsilon_fix not forwarded (mcts.py:50)
             v = float(scores[p2])
             n, q = N[best_i], Q[best_i]
             Q[best_i] = (n * q + v) / (n + 1)

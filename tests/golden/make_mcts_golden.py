@@ -119,7 +119,7 @@ def dump_tree(game: OracleGame, tree, root, max_nodes=48):
     return nodes
 
 
-def run_case(MCTS, preset, root, num_sims, cpuct, moves):
+def run_case(MCTS, preset, root, num_sims, cpuct, moves, epsilon_fix=True):
     o = Oracle(*preset)
     game = OracleGame(o)
     net = StubNet(game)
@@ -131,7 +131,7 @@ def run_case(MCTS, preset, root, num_sims, cpuct, moves):
             break
         player = Oracle.to_move(s)
         for _ in range(num_sims):
-            tree.simulate(s, player, cpuct=cpuct)
+            tree.simulate(s, player, cpuct=cpuct, epsilon_fix=epsilon_fix)
         d1 = tree.get_distribution(s, 1)
         d0 = tree.get_distribution(s, 0)
         a = int(d0[int(np.argmax(d0[:, 1])), 0][0])
@@ -146,7 +146,7 @@ def run_case(MCTS, preset, root, num_sims, cpuct, moves):
             "action": a,
         })
         s, _ = o.next_state(s, a)
-    return {"preset": list(preset), "cpuct": cpuct, "moves": out_moves}
+    return {"preset": list(preset), "cpuct": cpuct, "epsilon_fix": epsilon_fix, "moves": out_moves}
 
 
 def main():
@@ -162,11 +162,15 @@ def main():
         ((7, 2, 5), o7.random_board(3, 4), 150, 1, 3),
         ((7, 2, 5), o7.random_board(9, 6), 150, 3, 2),
         ((7, 2, 4), Oracle(7, 2, 4).init_state(), 100, 1, 2),
+        # simulate(..., epsilon_fix=False): sqrt(N.sum() + 0) at the root (mcts.py:43)
+        ((20, 4, 5), o20.init_state(), 40, 1, 2, False),
+        ((7, 2, 5), o7.random_board(3, 4), 150, 2, 2, False),
     ]
-    for k, (preset, root, sims, cpuct, moves) in enumerate(specs):
-        c = run_case(MCTS, preset, root, sims, cpuct, moves)
+    for k, (preset, root, sims, cpuct, moves, *eps) in enumerate(specs):
+        c = run_case(MCTS, preset, root, sims, cpuct, moves, *eps)
         nn = sum(len(m["nodes"]) for m in c["moves"])
-        print(f"case {k}: preset {preset} sims {sims} cpuct {cpuct} moves {len(c['moves'])} nodes {nn}")
+        print(f"case {k}: preset {preset} sims {sims} cpuct {cpuct} eps_fix {c['epsilon_fix']} "
+              f"moves {len(c['moves'])} nodes {nn}")
         cases.append(c)
     out = {
         "generator": "tests/golden/make_mcts_golden.py driving /root/reference/blokus_rl/alphazero/mcts.py",

@@ -95,7 +95,7 @@ class _StubNet:
         return self.o.make_state(cells, [0, 0, 0, 0], tm)
 
 
-@pytest.mark.parametrize("k", [0, 3, 6])
+@pytest.mark.parametrize("k", [0, 3, 6, 7, 8])
 def test_dropin_mcts_matches_reference(k, game20, game7):
     """MCTS.simulate / get_distribution called the way trainer._self_play calls them, with the
     reference-style predict() stub; distributions and root visit counts equal the golden
@@ -113,7 +113,7 @@ def test_dropin_mcts_matches_reference(k, game20, game7):
         s = state_of(mv["root"])
         p = g.to_move(s)
         for _ in range(mv["sims"]):
-            tree.simulate(s, p, cpuct=case["cpuct"])
+            tree.simulate(s, p, cpuct=case["cpuct"], epsilon_fix=case.get("epsilon_fix", True))
         d1 = tree.get_distribution(s, 1)
         d0 = tree.get_distribution(s, 0)
         assert [int(x[0]) for x in d1[:, 0]] == mv["ids"]

@@ -115,90 +115,3 @@ def test_leaf_resnet_head_operands_are_buffers():
     assert all(t.device.type == "cpu" for t in cpu.x3_heads) and cpu.x3_wtower.device.type == "cpu"
     back = cpu.to("cuda")
     assert all(t.is_cuda for t in back.x3_heads)
-
-
-@pytest.mark.parametrize("B,nblocks,kind", [(256, 5, "binary"), (7, 2, "dense"), (5, 1, "tiny"), (6, 2, "huge"),
-                                            (33, 5, "dense")])
-def test_leafnet_wx3_is_fp32_class(B, nblocks, kind):
-    """bk_leafnet_wx3 (the tower as Winograd F(2x2,3x3) on split-f16 products) against the fp64
-    forward, with the same bar as the direct x3 kernel: within 4x the f32 kernel's own error."""
-    from blokus_rl_amd.nets import LeafResNet, leafnet_wx3, resnet_stem_tower_heads
-
-    N = 20
-    net = _net(N, nblocks, seed=B + N + nblocks)
-    g = torch.Generator(device="cuda").manual_seed(B * 3 + N)
-    if kind == "binary":
-        obs = (torch.rand((B, 8, N, N), device="cuda", generator=g) < 0.3).float()
-    else:
-        scale = {"dense": 1.0, "tiny": 1e-3, "huge": 1e3}[kind]
-        obs = torch.randn((B, 8, N, N), device="cuda", generator=g) * scale
-    leaf = LeafResNet(net, normalize=False, features=True).eval()
-    pf, v, out = leafnet_wx3(obs, leaf, want_out=True)
-    pf32, v32 = resnet_stem_tower_heads(obs, leaf.w_stem_tower, leaf.u_tower, leaf.b_tower, 2 * nblocks, leaf.f)
-    torch.cuda.synchronize()
-    pf_ref, v_ref, xt_ref = _ref64(net, obs)
-    assert torch.isfinite(pf).all() and torch.isfinite(v).all()
-    e_w, e_32 = _rel(pf, pf_ref), _rel(pf32, pf_ref)
-    ev_w, ev_32 = float((v.double() - v_ref).abs().max()), float((v32.double() - v_ref).abs().max())
-    e_out = _rel(out, xt_ref)
-    print(f"wx3 {kind} B={B} blocks={nblocks}: pf {e_w:.3g} (f32 {e_32:.3g}) v {ev_w:.3g} (f32 {ev_32:.3g}) out {e_out:.3g}")
-    assert e_w <= max(4 * e_32, 2e-6), (e_w, e_32)
-    assert ev_w <= max(4 * ev_32, 2e-6), (ev_w, ev_32)
-    assert e_out <= 2e-6
-
-
-def test_leafnet_wx3_outputs_do_not_depend_on_the_batch():
-    from blokus_rl_amd.nets import LeafResNet, leafnet_wx3
-
-    net = _net(20, 2, seed=11)
-    leaf = LeafResNet(net, normalize=False, features=True).eval()
-    obs = (torch.rand((256, 8, 20, 20), device="cuda") < 0.3).float()
-    pf, v = leafnet_wx3(obs, leaf)
-    pf1, v1 = leafnet_wx3(obs[17:18].contiguous(), leaf)
-    assert torch.equal(pf[17:18], pf1) and torch.equal(v[17:18], v1)
-
-
-@pytest.mark.parametrize("B,nblocks,kind", [(256, 5, "binary"), (7, 2, "dense"), (5, 1, "tiny"), (6, 2, "huge"),
-                                            (33, 5, "dense")])
-def test_leafnet_x3g_is_fp32_class(B, nblocks, kind):
-    """bk_leafnet_x3g (the tower group-major, K split over wave pairs: each output the sum of two
-    half-K partial sums) against the fp64 forward with the x3 bar (within 4x the f32 kernel's own
-    error), and its tower output within fp32 rounding of bk_leafnet_x3's (the same products, the
-    two halves added at the end instead of in sequence)."""
-    from blokus_rl_amd.nets import LeafResNet, leafnet_x3, leafnet_x3g, resnet_stem_tower_heads
-
-    N = 20
-    net = _net(N, nblocks, seed=B + N + nblocks)
-    g = torch.Generator(device="cuda").manual_seed(B * 3 + N)
-    if kind == "binary":
-        obs = (torch.rand((B, 8, N, N), device="cuda", generator=g) < 0.3).float()
-    else:
-        scale = {"dense": 1.0, "tiny": 1e-3, "huge": 1e3}[kind]
-        obs = torch.randn((B, 8, N, N), device="cuda", generator=g) * scale
-    leaf = LeafResNet(net, normalize=False, features=True).eval()
-    pf, v, out = leafnet_x3g(obs, leaf, want_out=True)
-    pfx, vx, outx = leafnet_x3(obs, leaf, want_out=True)
-    pf32, v32 = resnet_stem_tower_heads(obs, leaf.w_stem_tower, leaf.u_tower, leaf.b_tower, 2 * nblocks, leaf.f)
-    torch.cuda.synchronize()
-    pf_ref, v_ref, xt_ref = _ref64(net, obs)
-    assert _rel(out, xt_ref) <= 2e-6
-    assert float((out - outx).abs().max()) <= 1e-5 * max(float(outx.abs().max()), 1e-30)
-    assert torch.isfinite(pf).all() and torch.isfinite(v).all()
-    e_g, e_x, e_32 = _rel(pf, pf_ref), _rel(pfx, pf_ref), _rel(pf32, pf_ref)
-    ev_g, ev_32 = float((v.double() - v_ref).abs().max()), float((v32.double() - v_ref).abs().max())
-    print(f"x3g {kind} B={B} blocks={nblocks}: pf {e_g:.3g} (x3 {e_x:.3g}, f32 {e_32:.3g}) v {ev_g:.3g} (f32 {ev_32:.3g})")
-    assert e_g <= max(4 * e_32, 2e-6), (e_g, e_32)
-    assert ev_g <= max(4 * ev_32, 2e-6), (ev_g, ev_32)
-
-
-def test_leafnet_x3g_outputs_do_not_depend_on_the_batch():
-    from blokus_rl_amd.nets import LeafResNet, leafnet_x3g
-
-    net = _net(20, 5, seed=13)
-    leaf = LeafResNet(net, normalize=False, features=True).eval()
-    obs = (torch.rand((256, 8, 20, 20), device="cuda") < 0.3).float()
-    pf, v = leafnet_x3g(obs, leaf)
-    pf1, v1 = leafnet_x3g(obs[17:18].contiguous(), leaf)
-    pf2, v2 = leafnet_x3g(obs, leaf)
-    assert torch.equal(pf[17:18], pf1) and torch.equal(v[17:18], v1)
-    assert torch.equal(pf, pf2) and torch.equal(v, v2)

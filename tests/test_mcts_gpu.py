@@ -23,7 +23,7 @@ CASES = load_cases()
 def _groups():
     g = defaultdict(list)
     for k, c in enumerate(CASES):
-        g[(tuple(c["preset"]), c["cpuct"])].append(k)
+        g[(tuple(c["preset"]), c["cpuct"], c.get("epsilon_fix", True))].append(k)
     return sorted(g.items())
 
 
@@ -38,12 +38,12 @@ def engines():
     return {p: Engine(*p) for p in {tuple(c["preset"]) for c in CASES}}
 
 
-@pytest.mark.parametrize("group", _groups(), ids=lambda g: f"{g[0][0]}-cpuct{g[0][1]}")
+@pytest.mark.parametrize("group", _groups(), ids=lambda g: f"{g[0][0]}-cpuct{g[0][1]}{'' if g[0][2] else '-noeps'}")
 def test_batched_mcts_matches_reference(engines, group):
     from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
     from oracle.oracle import Oracle
 
-    (preset, cpuct), case_ids = group
+    (preset, cpuct, eps_fix), case_ids = group
     eng = engines[preset]
     o = Oracle(*preset)
     dev = eng.device
@@ -61,7 +61,7 @@ def test_batched_mcts_matches_reference(engines, group):
         sims = [c["moves"][r]["sims"] if a else 0 for c, a in zip(cases, act_round)]
         for sim in range(max(sims)):
             active = torch.tensor([1 if sim < s else 0 for s in sims], dtype=torch.int32, device=dev)
-            status, _, mask = m.select(roots, active, float(cpuct))
+            status, _, mask = m.select(roots, active, float(cpuct), 1e-6 if eps_fix else 0.0)
             st_h = status.cpu().numpy()
             leaves, _ = m.leaf_info()
             leaves_h = leaves.cpu().numpy()

@@ -25,7 +25,7 @@ def test_mcts_oracle_matches_reference(k):
     for mv in case["moves"]:
         root = state_of(mv["root"])
         for _ in range(mv["sims"]):
-            r = m.simulate(root, cpuct=case["cpuct"])
+            r = m.simulate(root, cpuct=case["cpuct"], epsilon_fix=case.get("epsilon_fix", True))
         ids, d1 = m.get_distribution(root, 1)
         _, d0 = m.get_distribution(root, 0)
         assert ids.tolist() == mv["ids"]

@@ -21,10 +21,11 @@ pytestmark = pytest.mark.gpu
 T, SIMS, BLOCKS = 64, 100, 5
 
 
-def _dump_trees(sp, eng, o, roots_h):
-    """BFS over every tree through visited children: {tree: {hash: (state, ids, N, Q, P)}}."""
+def _dump_trees(sp, eng, o, roots_h, more=()):
+    """BFS over every tree through visited children from its root (and the roots in `more`):
+    {tree: {hash: (state, ids, N, Q, P)}}."""
     trees = [dict() for _ in range(T)]
-    frontier = [[roots_h[t]] for t in range(T)]
+    frontier = [[roots_h[t]] + [r[t] for r in more] for t in range(T)]
     cap = 2048
     while any(frontier):
         q = np.zeros((T, roots_h.shape[1]), dtype=np.uint8)
@@ -120,3 +121,78 @@ def test_config3_search_matches_oracle_replay():
         oids, d = m.get_distribution(roots_h[t], 1.0)
         K = int(rk[t])
         assert (rids[t, :K] == oids).all() and rpi[t, :K].tolist() == d.tolist(), t
+
+
+PLIES = 3
+
+
+def test_config3_tree_reuse_matches_oracle_replay():
+    """The production self-play plies (SelfPlay.play_ply: the captured simulation graph with
+    k_leaf_step_ov in continuous tree-reuse mode, then k_root / the fused ply tail picking each
+    game's move) for PLIES plies on 64 trees at config-3 shape (20x20, 5-block net, 100 sims), the
+    trees kept from ply to ply as the reference keeps one tree per episode (trainer.py:95,
+    102-128). Replayed through ONE persistent MCTSOracle per tree from the same roots with the
+    GPU's leaf evaluations: every node's N and float64 Q and each ply's root pi bit-exact after
+    every ply."""
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.boards import random_boards
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import ResNet, net_math
+
+    eng = Engine(20, 4, 5)
+    o = Oracle(20, 4, 5)
+    torch.manual_seed(0)
+    model = ResNet(20, 4, eng.A, num_res_blocks=BLOCKS).to(eng.device).eval()
+    sp = SelfPlay(eng, model, T, num_sims=SIMS, seed=3)
+    assert sp._graph_usable() and net_math() == "x3"
+    sp.roots = random_boards(eng, T, seed0=41, max_plies=24)
+    roots, dumps, pis = [], [], []
+    for _ in range(PLIES):
+        r = sp.roots.clone()
+        sp.play_ply()
+        sp.check()
+        # early-game roots (<= 24 plies played): no game can end inside the window, so no tree is
+        # reset and every root's node stays in its tree
+        assert bool(sp.active.all())
+        roots.append(r.cpu().numpy())
+        pis.append(tuple(x.cpu().numpy() for x in sp.mcts.root_policy(r, None, 1.0)))
+        # every root so far: a first-ply move drawn with Dirichlet noise may be an unvisited child
+        dumps.append(_dump_trees(sp, eng, o, roots[0], roots[1:]))
+    final = dumps[-1]
+
+    ev = sp.evaluator
+    keys = [(t, h) for t in range(T) for h in final[t]]
+    vals = {}
+    for i in range(0, len(keys), T):
+        chunk = keys[i:i + T]
+        st = np.zeros((T, roots[0].shape[1]), dtype=np.uint8)
+        for j, (t, h) in enumerate(chunk):
+            st[j] = final[t][h][0]
+        _, v = ev._forward(eng.observe(torch.from_numpy(st).to(eng.device)))
+        v = v.cpu().numpy()
+        for j, key in enumerate(chunk):
+            vals[key] = v[j].astype(np.float64)
+
+    for t in range(T):
+        nodes = final[t]
+
+        def evaluate(s, player, t=t, nodes=nodes):
+            h = o.hash(s)
+            _, ids, _, _, P = nodes[h]
+            assert (ids == o.legal_ids(s, player)).all()
+            return ids, P, vals[(t, h)]
+
+        m = MCTSOracle(o, evaluate)
+        for i in range(PLIES):
+            for _ in range(SIMS):
+                m.simulate(roots[i][t], cpuct=sp.cpuct)
+            snap = dumps[i][t]
+            assert set(m.tree) == set(snap), (t, i)
+            for h, nd in m.tree.items():
+                _, _, N, Q, _ = snap[h]
+                assert nd["N"] == N.tolist(), (t, i, h)
+                assert nd["Q"] == Q.tolist(), (t, i, h)
+            oids, d = m.get_distribution(roots[i][t], 1.0)
+            rids, rpi, rk = pis[i]
+            K = int(rk[t])
+            assert (rids[t, :K] == oids).all() and rpi[t, :K].tolist() == d.tolist(), (t, i)

@@ -1,7 +1,7 @@
-"""Whole simulations in one launch (bk_mcts_simulate_resnet / _const, sims.hip) against the
-per-stage launches they fuse (select -> leaf ResNet -> sparse policy head -> expand/backup, one
-launch each over all trees): the trees, counters and self-play plies come out bitwise identical.
-Also the captured simulation graph (SelfPlay.sim_graph_sims) against eager launches."""
+"""The fused leaf step (bk_mcts_leaf_step: sparse policy head + expand/backup + the next descent in
+one launch) against the per-stage launches it fuses (k_leaf_logits -> k_expand_backup ->
+k_select): the trees, counters and leaf outputs come out bitwise identical. Also the captured
+simulation graph (SelfPlay.sim_graph_sims) against eager launches."""
 import pytest
 import torch
 
@@ -14,41 +14,6 @@ def _leaf_model(eng, blocks=2, seed=0):
     torch.manual_seed(seed)
     net = ResNet(eng.N, eng.P, eng.A, blocks).cuda().eval()
     return LeafResNet(net, normalize=False, features=True).eval()
-
-
-@pytest.mark.parametrize("N,T,sims", [(20, 12, 9), (20, 5, 3), (14, 7, 6)])
-def test_fused_simulations_match_stagewise(N, T, sims, monkeypatch):
-    """k_sims<20> and k_sims<14> (the two board sizes the fused tower supports), against the
-    staged launches with the same (f32) net."""
-    monkeypatch.setenv("BK_NET_MATH", "f32")
-    from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
-    from blokus_rl_amd.boards import random_boards
-    from blokus_rl_amd.engine import Engine
-
-    eng = Engine(N, 4, 5)
-    model = _leaf_model(eng)
-    assert BatchedMCTS.fused_resnet_ok(eng, model)
-    roots = random_boards(eng, T, seed0=9, max_plies=24 if N == 20 else 12)
-    active = torch.ones(T, dtype=torch.int32, device=eng.device)
-    active[T // 2] = 0
-    kw = dict(node_cap=64, child_cap=T * 64 * 700)
-    m1, m2 = BatchedMCTS(eng, T, **kw), BatchedMCTS(eng, T, **kw)
-    po = model.f.policy_out
-    w, b = po.weight.detach().contiguous(), po.bias.detach().contiguous()
-    for _ in range(sims):
-        _, obs, _ = m1.select(roots, active, 1.5)
-        pf, v = model(obs)
-        m1.leaf_logits(pf.contiguous(), w, b)
-        m1.expand_backup(None, v.contiguous(), 2)
-    m2.simulate_resnet(roots, active, 1.5, sims, model)
-    c1, c2 = m1.check(), m2.check()
-    assert c1 == c2 and c1["expanded"] > 0
-    for x, y in zip(m1.root_stats(roots, active), m2.root_stats(roots, active)):
-        assert torch.equal(x, y)
-    s1, d1 = m1.leaf_info()
-    s2, d2 = m2.leaf_info()
-    a = active.bool()  # an inactive tree's leaf-state row is never written (uninitialised memory)
-    assert torch.equal(s1[a], s2[a]) and torch.equal(d1, d2)
 
 
 @pytest.mark.parametrize("N,T,sims,overlap", [(20, 12, 9, "1"), (20, 12, 9, "0"), (14, 7, 6, "1"), (20, 64, 40, "1")])
@@ -94,21 +59,17 @@ def test_leaf_step_matches_stagewise(N, T, sims, overlap, monkeypatch):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("fused,graph,gsims", [("1", "1", None), ("0", "1", None), ("0", "1", 10)])
-def test_selfplay_plies_match_eager(monkeypatch, fused, graph, gsims):
-    """The default play_ply paths (fused simulations, or the captured simulation graph: the whole
-    ply in one graph, or 10 per graph + eager rest) give the plies of launching every stage
-    eagerly."""
+@pytest.mark.parametrize("gsims", [None, 10])
+def test_selfplay_plies_match_eager(monkeypatch, gsims):
+    """The default play_ply path (the captured simulation graph: the whole ply in one graph, or 10
+    per graph + eager rest) gives the plies of launching every stage eagerly."""
     from blokus_rl_amd.alphazero.selfplay import SelfPlay
     from blokus_rl_amd.engine import Engine
     from blokus_rl_amd.nets import ResNet
 
     eng = Engine(20, 4, 5)
 
-    monkeypatch.setenv("BK_NET_MATH", "f32" if fused == "1" else "x3")
-
-    def run(f, g):
-        monkeypatch.setenv("BK_SIM_FUSED", f)
+    def run(g):
         monkeypatch.setenv("BK_SIM_GRAPH", g)
         torch.manual_seed(0)
         model = ResNet(20, 4, eng.A, num_res_blocks=2).to(eng.device).eval()
@@ -117,26 +78,23 @@ def test_selfplay_plies_match_eager(monkeypatch, fused, graph, gsims):
         for _ in range(3):
             sp.play_ply()
         _, n, q, p, k = sp.mcts.root_stats(sp.roots)
-        return (sp.roots.clone(), n, q, p, k), sp.mcts.check(), sp.fused()
+        return (sp.roots.clone(), n, q, p, k), sp.mcts.check()
 
-    ref, cref, fref = run("0", "0")
-    got, cgot, fgot = run(fused, graph)
-    assert not fref and fgot == (fused == "1")
+    ref, cref = run("0")
+    got, cgot = run("1")
     for x, y in zip(ref, got):
         assert torch.equal(x, y)
     assert cref == cgot
 
 
-@pytest.mark.parametrize("fused,graph", [("1", "1"), ("0", "1")])
-def test_dumbnet_plies_match_eager(monkeypatch, fused, graph):
+def test_dumbnet_plies_match_eager(monkeypatch):
     from blokus_rl_amd.alphazero.selfplay import SelfPlay
     from blokus_rl_amd.engine import Engine
     from blokus_rl_amd.nets import DumbNet
 
     eng = Engine(7, 2, 5)
 
-    def run(f, g):
-        monkeypatch.setenv("BK_SIM_FUSED", f)
+    def run(g):
         monkeypatch.setenv("BK_SIM_GRAPH", g)
         sp = SelfPlay(eng, DumbNet(7, 2, eng.A), 16, num_sims=24, node_cap=2048, seed=3)
         for _ in range(4):
@@ -144,8 +102,8 @@ def test_dumbnet_plies_match_eager(monkeypatch, fused, graph):
         _, n, q, p, k = sp.mcts.root_stats(sp.roots, sp.active)
         return (sp.roots.clone(), n, q, k), sp.mcts.check()
 
-    ref, cref = run("0", "0")
-    got, cgot = run(fused, graph)
+    ref, cref = run("0")
+    got, cgot = run("1")
     for x, y in zip(ref, got):
         assert torch.equal(x, y)
     assert cref == cgot

@@ -10,10 +10,9 @@ mkdir -p "$obj" blokus_rl_amd/_lib/exp
 rm -f "$obj"/*.o
 cd "$src"
 pids=()
-for f in env.hip mcts.hip vecenv.hip train.hip ppo.hip netops.hip conv.hip sims.hip leafnet.hip leafnet_wino.hip leafnet_g.hip ply.hip; do
+for f in env.hip mcts.hip vecenv.hip train.hip ppo.hip netops.hip conv.hip leafnet.hip ply.hip; do
   [ -f "$f" ] || continue
-  XF=""; [ "$f" = conv.hip ] || [ "$f" = sims.hip ] && XF="-fno-slp-vectorize"
-  [ "$f" = leafnet_wino.hip ] && XF="-fno-slp-vectorize -ffp-contract=fast"
+  XF=""; [ "$f" = conv.hip ] && XF="-fno-slp-vectorize"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function $XF $flags \
     -c -o "$obj/$f.o" $f &
   pids+=($!)
