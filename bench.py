@@ -394,9 +394,11 @@ def cpu_baseline_legal(states: torch.Tensor, seconds: float, pool=None, workers:
                       f"processes, repeated) in {dt:.1f} s"}
 
 
-# Config 5 algorithmic bytes per env-step: state read + write (768), action (4), rng (16),
-# obs (49 u8), mask (15 u64 = 120 at 919 ids), reward + done (8). DESIGN.md §4.
-VEC_BYTES_PER_STEP = 768 + 4 + 16 + 49 + 120 + 8
+# Config 5 bytes per env-step as k_vec_step7 moves them: the state words a 2-colour 7x7 game uses,
+# read and written (occupancy rows 0..7 of colours 0 and 1, pieces, hash / to-move / ply, flags:
+# 100 B each way), rng (16), obs (49 u8), mask (15 u64 = 120 at 919 ids), reward + done (8); the
+# benchmark's agent draws in-kernel (no action read). DESIGN.md §4.
+VEC_BYTES_PER_STEP = 100 + 100 + 16 + 49 + 120 + 8
 
 
 def bench_vecenv(args, world, rank):
@@ -439,7 +441,7 @@ def bench_vecenv(args, world, rank):
            "value": E * args.vec_steps * world / dt, "unit": "env-steps/s", "envs_per_gpu": E,
            "steps": args.vec_steps,
            "with_masked_policy_sampling": {"value": E * n2 / dt2, "unit": "env-steps/s"},
-           "roofline": {"bound": "hbm", "kernel": "k_vec_step", "achieved": achieved / 1e9,
+           "roofline": {"bound": "hbm", "kernel": "k_vec_step7", "achieved": achieved / 1e9,
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
                         "kernel_ms": kernel_ms, "bytes_per_unit": VEC_BYTES_PER_STEP, "units_per_launch": E}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

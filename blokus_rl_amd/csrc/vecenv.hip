@@ -13,6 +13,9 @@
 // same function in oracle/vecenv_oracle.py, so trajectories compare bit for bit.
 #include "../../include/blokus_engine.h"
 #include "ctx.h"
+#include "orient_table.h"
+
+#include <cstdlib>
 
 namespace bk {
 namespace {
@@ -147,6 +150,382 @@ __global__ __launch_bounds__(64) void k_vec_step(DevPreset dp, uint32_t* states,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_vec_step7: the same step for the 7x7 presets (config 5), EIGHT lanes per env instead of a
+// wave. A 7x7 colour is one u64 bitboard with rows at stride 8 (bit 8 r + c; column 7 is a guard
+// that absorbs the +-1 column shifts), so a colour's forbidden / anchor cells are a handful of
+// 64-bit shifts and the legal origins of a fixed orientation are
+//   L_o = VALID_o & ~OR_k (F >> off_k) & OR_k (A >> off_k)      (off_k = 8 dr_k + dc_k)
+// (compute_fa + eval_item of common.h on whole boards). The orientations are dealt round robin
+// to the 8 lanes of an env (orientation 8 i + j to lane j: 4 per lane for the 919-id preset, 12
+// for the 2522-id one), each lane holding its orientations' cells / valid origins / id base in
+// registers. Counting, the k-th legal id (ascending id = ascending orientation, then origin bit
+// r*8 + c, as the bitmask order), hash updates and the legal-move mask are per-lane work met by
+// 3-step DPP butterflies inside the octet; obs and mask are staged in LDS and leave as coalesced
+// rows. Only the state words a 2-colour 7x7 game uses are read and written (occupancy rows 0..6
+// of colours 0 and 1, pieces, hash, to-move, ply, flags); the rest of the 384-B state stays as
+// bk_vec_reset wrote it (zero). Bitwise the trajectories of k_vec_step (tests/test_vecenv_gpu.py).
+constexpr uint64_t kBoard7 = 0x007F7F7F7F7F7F7Full;  // rows 0..6 x columns 0..6 at stride 8
+constexpr int kVecThreads = 256, kVecEnvsPerBlock = kVecThreads / 8;
+
+template <int MC>
+struct Vec7 {
+  static constexpr int NO = MC == 4 ? 28 : 91;     // fixed orientations of the <= MC-cell pieces
+  static constexpr int NP = MC == 4 ? 9 : 21;      // pieces
+  static constexpr int NL = (NO + 7) / 8;          // orientations per lane
+  static constexpr int A = MC == 4 ? 919 : 2522;   // action ids
+  static constexpr int W64 = (A + 63) / 64, W32 = (A + 31) / 32;
+};
+// per orientation: cells at stride 8 packed 6 bits each (unused cells repeat cell 0), valid
+// origins, first id | piece << 12 | origin columns W << 17 | height h << 20
+struct Or7 {
+  uint32_t offs, meta;
+  uint64_t valid;
+};
+template <int MC>
+struct Or7Table {
+  Or7 o[Vec7<MC>::NO];
+  constexpr Or7Table() : o() {
+    int id = 0;
+    for (int k = 0; k < Vec7<MC>::NO; ++k) {
+      const OrientC& q = kOrient[k];
+      uint32_t offs = 0;
+      for (int i = 0; i < 5; ++i) offs |= (uint32_t)(q.dr[i] * 8 + q.dc[i]) << (6 * i);
+      const int R = 8 - q.h, W = 8 - q.w;
+      uint64_t valid = 0;
+      for (int r = 0; r < R; ++r)
+        for (int c = 0; c < W; ++c) valid |= 1ull << (r * 8 + c);
+      o[k] = Or7{offs, (uint32_t)id | ((uint32_t)q.piece << 12) | ((uint32_t)W << 17) | ((uint32_t)q.h << 20), valid};
+      id += R * W;
+    }
+  }
+};
+template <int MC>
+__device__ constexpr Or7Table<MC> kOr7{};
+
+// octet (8-lane) collectives on DPP: quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int oct_sum(int x) {
+  x += (int)dppu<0xB1>((uint32_t)x);
+  x += (int)dppu<0x4E>((uint32_t)x);
+  x += (int)dppu<0x141>((uint32_t)x);
+  return x;
+}
+__device__ __forceinline__ uint64_t oct_or64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  lo |= dppu<0xB1>(lo);
+  hi |= dppu<0xB1>(hi);
+  lo |= dppu<0x4E>(lo);
+  hi |= dppu<0x4E>(hi);
+  lo |= dppu<0x141>(lo);
+  hi |= dppu<0x141>(hi);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t oct_xor64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  lo ^= dppu<0xB1>(lo);
+  hi ^= dppu<0xB1>(hi);
+  lo ^= dppu<0x4E>(lo);
+  hi ^= dppu<0x4E>(hi);
+  lo ^= dppu<0x141>(lo);
+  hi ^= dppu<0x141>(hi);
+  return ((uint64_t)hi << 32) | lo;
+}
+// inclusive prefix sum over lanes 0..j of the octet (row_shr 1, 2, 4 inside each 8-lane segment)
+__device__ __forceinline__ int oct_incl(int x, int j) {
+  int t = (int)dppu<0x111>((uint32_t)x);
+  if (j >= 1) x += t;
+  t = (int)dppu<0x112>((uint32_t)x);
+  if (j >= 2) x += t;
+  t = (int)dppu<0x114>((uint32_t)x);
+  if (j >= 4) x += t;
+  return x;
+}
+// bit index of the k-th (0-based) set bit of x (k < popcount(x)): binary search on popcounts
+__device__ __forceinline__ int kth_bit64(uint64_t x, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t lo = x & ((1ull << w) - 1ull);
+    const int c = __popcll(lo);
+    if (k >= c) {
+      k -= c;
+      x >>= w;
+      pos += w;
+    } else {
+      x = lo;
+    }
+  }
+  return pos;
+}
+
+template <int MC>
+__global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uint64_t* rng,
+                                                          const int32_t* __restrict__ actions, int E,
+                                                          uint8_t* __restrict__ obs, uint64_t* __restrict__ mask,
+                                                          float* __restrict__ reward, int32_t* __restrict__ done) {
+  using V = Vec7<MC>;
+  constexpr int NL = V::NL;
+  __shared__ uint32_t m32[kVecEnvsPerBlock][V::W32 + 1];
+  __shared__ __attribute__((aligned(16))) uint8_t ob[kVecEnvsPerBlock * 49 + 16];
+  const int tid = threadIdx.x, j = tid & 7, le = tid >> 3;
+  const int e0 = blockIdx.x * kVecEnvsPerBlock;
+  const int e = e0 + le;
+  const bool live = e < E;
+  const int es = live ? e : E - 1;  // a spare octet mirrors the last env and stores nothing
+
+  // this lane's orientations (8 i + j): cells, valid origins, meta
+  uint32_t offs[NL], meta[NL];
+  uint64_t valid[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int k = 8 * i + j;
+    const Or7 q = kOr7<MC>.o[k < V::NO ? k : 0];
+    offs[i] = q.offs;
+    meta[i] = q.meta;
+    valid[i] = k < V::NO ? q.valid : 0ull;
+  }
+  // the state words of a 7x7 / 2-colour game
+  const uint32_t* g = states + (size_t)es * kStateWords;
+  uint64_t occ[2];
+  {
+    const uint4 a0 = *reinterpret_cast<const uint4*>(g), a1 = *reinterpret_cast<const uint4*>(g + 4);
+    const uint4 b0 = *reinterpret_cast<const uint4*>(g + kMaxN), b1 = *reinterpret_cast<const uint4*>(g + kMaxN + 4);
+    occ[0] = (uint64_t)a0.x | (uint64_t)a0.y << 8 | (uint64_t)a0.z << 16 | (uint64_t)a0.w << 24 |
+             (uint64_t)a1.x << 32 | (uint64_t)a1.y << 40 | (uint64_t)a1.z << 48;
+    occ[1] = (uint64_t)b0.x | (uint64_t)b0.y << 8 | (uint64_t)b0.z << 16 | (uint64_t)b0.w << 24 |
+             (uint64_t)b1.x << 32 | (uint64_t)b1.y << 40 | (uint64_t)b1.z << 48;
+  }
+  const uint4 w80 = *reinterpret_cast<const uint4*>(g + kWPieces);  // pieces of colours 0..3
+  const uint4 w84 = *reinterpret_cast<const uint4*>(g + kWHash);    // hash lo, hi, to-move, ply
+  uint32_t pieces[2] = {w80.x, w80.y};
+  uint64_t hash = (uint64_t)w84.x | ((uint64_t)w84.y << 32);
+  int to_move = (int)w84.z;
+  uint32_t ply = w84.w, flags = g[kWFlags];
+  uint64_t st = rng[es];
+
+  // legal origins of colour q for this lane's orientations into L; returns the env's legal-move
+  // count (also kept in lastK)
+  uint64_t L[NL];
+  int lastK = 0;
+  auto legal = [&](int q) {
+    const uint64_t own = occ[q], all = occ[0] | occ[1];
+    const uint64_t F = all | own << 1 | own >> 1 | own << 8 | own >> 8;
+    const uint64_t A = own ? ((own << 9 | own << 7 | own >> 7 | own >> 9) & kBoard7) : (q == 0 ? 1ull : 1ull << 54);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      uint64_t fo = 0, ao = 0;
+#pragma unroll
+      for (int k = 0; k < MC; ++k) {  // cells past the piece's size repeat cell 0
+        const int off = (int)((offs[i] >> (6 * k)) & 63u);
+        fo |= F >> off;
+        ao |= A >> off;
+      }
+      const bool have = (pieces[q] >> ((meta[i] >> 12) & 31u)) & 1u;
+      L[i] = have ? (valid[i] & ~fo & ao) : 0ull;
+      cnt += __popcll(L[i]);
+    }
+    lastK = oct_sum(cnt);
+    return lastK;
+  };
+  // the k-th legal id in ascending order -> (id, the orientation's offs, meta, origin bit), the
+  // same in every lane of the octet
+  struct Pick {
+    int id;
+    uint32_t offs, meta;
+    int org;
+  };
+  auto kth = [&](int k) {
+    int before = 0;
+    uint64_t sel = 0;  // id | org << 16 from the owning lane
+    uint32_t so = 0, sm = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = __popcll(L[i]);
+      const int incl = oct_incl(c, j), tot = oct_sum(c);
+      const int kk = k - before - (incl - c);
+      if (kk >= 0 && kk < c) {
+        const int pos = kth_bit64(L[i], kk);
+        const int W = (int)((meta[i] >> 17) & 7u);
+        const int id = (int)(meta[i] & 0xFFFu) + (pos >> 3) * W + (pos & 7);
+        sel = (uint64_t)(uint32_t)id | ((uint64_t)(uint32_t)pos << 16) | (1ull << 63);
+        so = offs[i];
+        sm = meta[i];
+      }
+      before += tot;
+    }
+    sel = oct_or64(sel);
+    const uint64_t om = oct_or64(((uint64_t)sm << 32) | so);
+    return Pick{(int)(sel & 0xFFFFu), (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 16) & 63u)};
+  };
+  // decode a given id -> the same Pick; id -1 when it is out of range or not a legal origin of the
+  // colour whose origins L holds (the owning lane tests its bit)
+  auto decode = [&](int a) {
+    uint64_t sel = 0;
+    uint32_t so = 0, sm = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u), h = (int)((meta[i] >> 20) & 7u);
+      const int rel = a - base;
+      if (valid[i] && rel >= 0 && rel < (8 - h) * W) {
+        const int r = rel / W, c = rel - r * W;
+        if ((L[i] >> (r * 8 + c)) & 1ull) {
+          sel = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)(r * 8 + c) << 16) | (1ull << 63);
+          so = offs[i];
+          sm = meta[i];
+        }
+      }
+    }
+    sel = oct_or64(sel);
+    const uint64_t om = oct_or64(((uint64_t)sm << 32) | so);
+    return Pick{(sel >> 63) ? (int)(sel & 0xFFFFu) : -1, (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 16) & 63u)};
+  };
+  // place pick p for colour q: cells, pieces, ply, the board hash (rows r.. r+h-1, one lane each)
+  auto place = [&](int q, const Pick& p) {
+    uint64_t cells = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) cells |= 1ull << ((p.offs >> (6 * k)) & 63u);
+    cells <<= p.org;
+    const uint64_t before = occ[q], after = before | cells;
+    const int r0 = p.org >> 3, h = (int)((p.meta >> 20) & 7u), row = r0 + j;
+    uint64_t hx = 0;
+    if (j < h) {
+      const uint32_t o = (uint32_t)(before >> (8 * row)) & 0x7Fu, nw = (uint32_t)(after >> (8 * row)) & 0x7Fu;
+      hx = (o ? row_key(q, row, o) : 0ull) ^ row_key(q, row, nw);
+    }
+    hash ^= oct_xor64(hx);
+    occ[q] = after;
+    pieces[q] &= ~(1u << ((p.meta >> 12) & 31u));
+    ply += 1u;
+  };
+  // advance_turn (common.h) after colour p placed; last_q: the colour whose L the last legal()
+  // call left (-1 none): the next mover's origins stay in L for the caller
+  int last_q = -1;
+  auto advance = [&](int p) {
+    int next = -1;
+    for (int d = 1; d <= 2; ++d) {
+      const int q = (p + d) & 1;
+      if ((flags >> (kFlagDeadShift + q)) & 1u) continue;
+      const int K = legal(q);
+      last_q = q;
+      if (K > 0) {
+        next = q;
+        break;
+      }
+      flags |= 1u << (kFlagDeadShift + q);
+    }
+    if (next < 0) {
+      flags |= kFlagOver;
+      next = (p + 1) & 1;
+      last_q = -1;
+    }
+    to_move = next;
+  };
+
+  float rew = 0.0f;
+  int fin = 0;
+  const int a = actions ? actions[es] : -1;
+  const int K0 = legal(0);  // the agent (colour 0) is to move at every step start
+  // the agent's move: the given id if it is legal, else (a < 0) a uniformly random legal one
+  Pick pk = a >= 0 ? decode(a) : (K0 > 0 ? kth((int)rng_index(&st, K0)) : Pick{-1, 0u, 0u, 0});
+  if (pk.id < 0) {  // an illegal agent action (or no legal move) ends the episode as a loss
+    rew = -1.0f;
+    fin = 1;
+  } else {
+    place(0, pk);
+    advance(0);
+    // the built-in random opponent moves while it is colour 1's turn (advance left its origins in L)
+    while (!(flags & kFlagOver) && to_move == 1) {
+      const Pick pb = kth((int)rng_index(&st, lastK));
+      place(1, pb);
+      advance(1);
+    }
+    if (flags & kFlagOver) {
+      const int a0 = __popcll(occ[0]), a1 = __popcll(occ[1]);
+      rew = a0 > a1 ? 1.0f : (a0 < a1 ? -1.0f : 0.0f);
+      fin = 1;
+    }
+  }
+  if (fin) {  // auto-reset (gymnasium vector-env semantics): init_state_lds's words
+    occ[0] = occ[1] = 0ull;
+    pieces[0] = pieces[1] = (1u << V::NP) - 1u;
+    hash = 0x9E3779B97F4A7C15ull;
+    to_move = 0;
+    ply = 0u;
+    flags = 0u;
+    last_q = -1;
+  }
+  if (last_q != 0) legal(0);  // the agent's legal origins for its mask
+
+  // ---- outputs: the state words, rng, reward, done (lane 0 of the octet); obs and mask via LDS
+  for (int w = tid; w < kVecEnvsPerBlock * (V::W32 + 1); w += kVecThreads) (&m32[0][0])[w] = 0u;
+  __syncthreads();
+  if (live) {
+    uint32_t* gs = states + (size_t)e * kStateWords;
+    if (j == 0) {
+      *reinterpret_cast<uint4*>(gs) = make_uint4((uint32_t)occ[0] & 0x7Fu, (uint32_t)(occ[0] >> 8) & 0x7Fu,
+                                                 (uint32_t)(occ[0] >> 16) & 0x7Fu, (uint32_t)(occ[0] >> 24) & 0x7Fu);
+      *reinterpret_cast<uint4*>(gs + 4) = make_uint4((uint32_t)(occ[0] >> 32) & 0x7Fu, (uint32_t)(occ[0] >> 40) & 0x7Fu,
+                                                     (uint32_t)(occ[0] >> 48) & 0x7Fu, 0u);
+    } else if (j == 1) {
+      *reinterpret_cast<uint4*>(gs + kMaxN) = make_uint4((uint32_t)occ[1] & 0x7Fu, (uint32_t)(occ[1] >> 8) & 0x7Fu,
+                                                         (uint32_t)(occ[1] >> 16) & 0x7Fu,
+                                                         (uint32_t)(occ[1] >> 24) & 0x7Fu);
+      *reinterpret_cast<uint4*>(gs + kMaxN + 4) =
+          make_uint4((uint32_t)(occ[1] >> 32) & 0x7Fu, (uint32_t)(occ[1] >> 40) & 0x7Fu,
+                     (uint32_t)(occ[1] >> 48) & 0x7Fu, 0u);
+    } else if (j == 2) {
+      *reinterpret_cast<uint4*>(gs + kWPieces) = make_uint4(pieces[0], pieces[1], 0u, 0u);
+      *reinterpret_cast<uint4*>(gs + kWHash) = make_uint4((uint32_t)hash, (uint32_t)(hash >> 32), (uint32_t)to_move, ply);
+      gs[kWFlags] = flags;
+    } else if (j == 3) {
+      rng[e] = st;
+      reward[e] = rew;
+      done[e] = fin;
+    }
+    // obs: lane j < 7 writes row j (0 empty, 1 colour 0, 2 colour 1)
+    if (j < 7) {
+      const uint32_t r0 = (uint32_t)(occ[0] >> (8 * j)) & 0x7Fu, r1 = (uint32_t)(occ[1] >> (8 * j)) & 0x7Fu;
+#pragma unroll
+      for (int c = 0; c < 7; ++c) ob[le * 49 + j * 7 + c] = ((r0 >> c) & 1u) ? 1 : (((r1 >> c) & 1u) ? 2 : 0);
+    }
+    // mask: each legal origin row of the lane's orientations ORed into the env's LDS words
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      uint64_t x = L[i];
+      const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u);
+      while (x) {
+        const int r = (__ffsll((unsigned long long)x) - 1) >> 3;
+        const uint32_t bits = (uint32_t)(x >> (8 * r)) & 0x7Fu;
+        x &= ~(0xFFull << (8 * r));
+        const int pos = base + r * W, w = pos >> 5, sh = pos & 31;
+        atomicOr(&m32[le][w], bits << sh);
+        if (sh + W > 32) atomicOr(&m32[le][w + 1], bits >> (32 - sh));
+      }
+    }
+  }
+  __syncthreads();
+  // the block's envs are contiguous: obs rows as dwords, mask rows as u64 (coalesced)
+  const int nenv = min(kVecEnvsPerBlock, E - e0);
+  {
+    uint8_t* o = obs + (size_t)e0 * 49;  // 16-B aligned: e0 * 49 is a multiple of 32 * 49 = 98 x 16
+    if (nenv == kVecEnvsPerBlock) {
+      if (tid < kVecEnvsPerBlock * 49 / 16)
+        reinterpret_cast<uint4*>(o)[tid] = reinterpret_cast<const uint4*>(ob)[tid];
+    } else {
+      for (int i = tid; i < nenv * 49; i += kVecThreads) o[i] = ob[i];
+    }
+  }
+  for (int i = tid; i < nenv * V::W64; i += kVecThreads) {
+    const int le2 = i / V::W64, w = i - le2 * V::W64;
+    mask[(size_t)(e0 + le2) * V::W64 + w] = (uint64_t)m32[le2][2 * w] | ((uint64_t)m32[le2][2 * w + 1] << 32);
+  }
+}
+
 }  // namespace
 }  // namespace bk
 
@@ -175,6 +554,17 @@ int bk_vec_step(bk_ctx* c, void* states, uint64_t* rng, const int32_t* actions, 
   BK_REQUIRE(c->d_items, "host-only context (created with device < 0)");
   BK_REQUIRE(c->dp.P == 2, "the vector env is the 2-player preset");
   if (E == 0) return BK_OK;
+  const char* g = getenv("BK_VEC_WAVE");  // A/B: the one-wave-per-env kernel on 7x7 too
+  if (c->dp.N == 7 && (c->dp.num_pieces == 9 || c->dp.num_pieces == 21) && !(g && atoi(g))) {
+    const dim3 grid((E + kVecEnvsPerBlock - 1) / kVecEnvsPerBlock);
+    if (c->dp.num_pieces == 9)
+      hipLaunchKernelGGL(k_vec_step7<4>, grid, dim3(kVecThreads), 0, (hipStream_t)stream, (uint32_t*)states, rng,
+                         actions, E, obs, mask, reward, done);
+    else
+      hipLaunchKernelGGL(k_vec_step7<5>, grid, dim3(kVecThreads), 0, (hipStream_t)stream, (uint32_t*)states, rng,
+                         actions, E, obs, mask, reward, done);
+    return launch_check("k_vec_step7");
+  }
   hipLaunchKernelGGL(k_vec_step, dim3(E), dim3(kWave), vec_lds(c->dp), (hipStream_t)stream, c->dp,
                      (uint32_t*)states, rng, actions, obs, mask, reward, done);
   return launch_check("k_vec_step");
