@@ -57,6 +57,16 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 #ifndef BK_LN_WPF
 #define BK_LN_WPF 1  // chunks of weight read-ahead (A/B knob: 1 or 2)
 #endif
+#ifndef BK_LN_VACC
+#define BK_LN_VACC 0  // A/B knob: the MFMA accumulators in VGPRs (1) or AGPRs (0)
+#endif
+#if BK_LN_VACC
+#define BK_ACC_W "=&v"
+#define BK_ACC_RW "+v"
+#else
+#define BK_ACC_W "=&a"
+#define BK_ACC_RW "+a"
+#endif
 constexpr int kLnPf = BK_LN_PF, kLnSlots = 5, kLnWpf = BK_LN_WPF;
 static_assert(kLnPf >= 1 && kLnPf < kLnSlots, "BK_LN_PF");
 __host__ __device__ constexpr int ln_groups(int N) { return ((N * N + 15) / 16 + kLnSlots - 1) / kLnSlots * kLnSlots; }
@@ -239,14 +249,14 @@ __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, c
           "v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\t"
           "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
           "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
-          : "=&a"(acc[g])
+          : BK_ACC_W(acc[g])
           : "v"(ah), "v"(bh), "v"(al), "v"(bl));
     else
       asm volatile(
           "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
           "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
           "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
-          : "+a"(acc[g])
+          : BK_ACC_RW(acc[g])
           : "v"(ah), "v"(bh), "v"(al), "v"(bl));
   }
 }
@@ -259,7 +269,7 @@ template <int NG>
 __device__ __forceinline__ void ln_mfma_drain(f32x4 (&acc)[NG]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
-  for (int g = 0; g < NG; ++g) asm volatile("" : "+a"(acc[g]));
+  for (int g = 0; g < NG; ++g) asm volatile("" : BK_ACC_RW(acc[g]));
 }
 
 struct LnHeads {

@@ -14,3 +14,16 @@ timeout -k 10 300 python bench.py --workload vecenv --no-cpu-baseline > gpurun_o
 cut -c1-400 gpurun_out/lnp/vec.json
 BK_VEC_WAVE=1 timeout -k 10 300 python bench.py --workload vecenv --no-cpu-baseline > gpurun_out/lnp/vec_wave.json 2> gpurun_out/lnp/vec.err || { tail gpurun_out/lnp/vec.err; exit 1; }
 cut -c1-300 gpurun_out/lnp/vec_wave.json
+# VGPR accumulators in the 4-wave kernel (libvacc.so) vs the shipped AGPR form: bitwise + time
+timeout -k 10 120 python tools/leafnet_ab.py dump gpurun_out/lnp/base.pt > gpurun_out/lnp/dump.log 2>&1 || exit 1
+BK_LIB=blokus_rl_amd/_lib/exp/libvacc.so timeout -k 10 120 python tools/leafnet_ab.py dump gpurun_out/lnp/vacc.pt >> gpurun_out/lnp/dump.log 2>&1 || exit 1
+python tools/leafnet_ab.py cmp gpurun_out/lnp/base.pt gpurun_out/lnp/vacc.pt
+for i in 1 2; do
+  timeout -k 10 120 python tools/leafnet_bench.py 200 256 2>> gpurun_out/lnp/time.err | sed 's/^/agpr /' || exit 1
+  BK_LIB=blokus_rl_amd/_lib/exp/libvacc.so timeout -k 10 120 python tools/leafnet_bench.py 200 256 2>> gpurun_out/lnp/time.err | sed 's/^/vacc /' || exit 1
+done
+# per-tree phases of k_leaf_step_ov mid-game (diag build): median vs slowest tree
+for p in 8 16; do
+  BK_LIB=blokus_rl_amd/_lib/diag/libblokus_hip_diag.so timeout -k 10 300 python tools/stamp_step_ov.py $p > gpurun_out/lnp/step_ov_$p.json 2>> gpurun_out/lnp/step.err || { tail gpurun_out/lnp/step.err; exit 1; }
+  cut -c1-700 gpurun_out/lnp/step_ov_$p.json
+done
