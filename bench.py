@@ -402,7 +402,9 @@ VEC_BYTES_PER_STEP = 100 + 100 + 16 + 49 + 120 + 8
 
 
 def bench_vecenv(args, world, rank):
-    """Config 5: the PPO 7x7 vector env, E envs, one fused k_vec_step launch per vector step."""
+    """Config 5: the PPO 7x7 vector env, E envs, one fused k_vec_step7 launch per vector step;
+    `value` from steps replayed out of a captured HIP graph (the device rate), plus the same steps
+    called eagerly through env.step() and with masked policy sampling."""
     from blokus_rl_amd.vector_env import BlokusVectorEnv
 
     E = args.envs
@@ -410,19 +412,37 @@ def bench_vecenv(args, world, rank):
     env.reset(seed=rank)
     stream = torch.cuda.current_stream()
     for _ in range(20):
-        env.step(None)
+        env.step_raw(None)
     torch.cuda.synchronize()
+    # the device step rate: the steps replayed from a HIP graph of `per` captured launches (the
+    # host's per-call launch cost would otherwise set the rate of a ~10 us kernel)
+    per = 25
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per):
+            env.step_raw(None)
+    g.replay()
+    torch.cuda.synchronize()
+    reps = max(1, args.vec_steps // per)
     _barrier(world)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.vec_steps):
-        env.step(None)  # in-kernel random agent (policy stand-in), then the random opponent
+    for _ in range(reps):
+        g.replay()  # in-kernel random agent (policy stand-in), then the random opponent
     e1.record(stream)
     torch.cuda.synchronize()
     _barrier(world)
     dt = _max_over_ranks(time.perf_counter() - t0, world)
-    kernel_ms = e0.elapsed_time(e1) / args.vec_steps
+    steps_done = reps * per
+    kernel_ms = e0.elapsed_time(e1) / steps_done
+    # the same steps launched eagerly from Python, one env.step() call each (gymnasium-style API)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    for _ in range(200):
+        env.step(None)
+    torch.cuda.synchronize()
+    eager = E * 200 / (time.perf_counter() - te)
     # PPO-style: the agent's actions sampled on the device from masked logits each step
     logits = torch.zeros((E, env.eng.A), device=env.device)
     for _ in range(5):
@@ -438,8 +458,8 @@ def bench_vecenv(args, world, rank):
     dt2 = time.perf_counter() - t1
     achieved = VEC_BYTES_PER_STEP * E / (kernel_ms * 1e-3)
     out = {"metric": "PPO vector-env steps/sec (7x7, 2 players, 919 ids, random opponent)",
-           "value": E * args.vec_steps * world / dt, "unit": "env-steps/s", "envs_per_gpu": E,
-           "steps": args.vec_steps,
+           "value": E * steps_done * world / dt, "unit": "env-steps/s", "envs_per_gpu": E,
+           "steps": steps_done, "eager_env_step_calls": {"value": eager * world, "unit": "env-steps/s"},
            "with_masked_policy_sampling": {"value": E * n2 / dt2, "unit": "env-steps/s"},
            "roofline": {"bound": "hbm", "kernel": "k_vec_step7", "achieved": achieved / 1e9,
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,

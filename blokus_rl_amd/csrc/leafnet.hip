@@ -29,9 +29,6 @@
 
 #include "leafnet_common.h"
 
-#include <cstdlib>
-#include <type_traits>
-
 namespace bk {
 namespace {
 
@@ -441,508 +438,6 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 
 static_assert(ln_lds_bytes(20) <= 160 * 1024, "k_leafnet_x3<20>: LDS");
 
-// ---------------------------------------------------------------------------------------------
-// k_leafnet_x3p: the same network, the same products in the same order (bitwise the outputs of
-// the 4-wave form above), with TWO waves per SIMD so that one wave's epilogue (VALU + LDS stores,
-// ~17% of a layer with the matrix cores idle in the 4-wave form) runs while its SIMD partner
-// issues MFMAs.
-//
-// 8 waves: wave w computes output channels 16 (w % 4).. of the board HALF w / 4 (rows 0..N/2-1 or
-// N/2..N-1; kLnHalfMap: NGH groups of 16 pixels per half, bank-conflict-free as LnPixMap). The two
-// waves of a SIMD thus share the weights and split the pixels. The halves are skewed by about half
-// a layer, and the skew is legal because of where a half reads the other half's rows: the top
-// half's bottom row reads the row below only in taps 6..8 (K chunks 12..17), the bottom half's top
-// row reads the row above only in taps 0..2 (chunks 0..5). Four workgroup barriers per conv L
-// order everything (both halves pass the same sequence P X Q R P X Q R ...):
-//
-//   top    [P_L] c0..c9 [X_L-1] c10..c11 [Q_L] c12..c17 epilogue [R_L] write x_L+1 [P_L+1]
-//   bottom [P_L] c10..c17 of conv L-1, epilogue [X_L-1] write x_L [Q_L] c0..c7 [R_L] c8..c9 [P_L+1]
-//
-// RAW: top reads its rows of x_L after P_L (its writes before), row N/2 after Q_L (bottom's writes
-// between X_L-1 and Q_L); bottom reads row N/2-1 in c0..c5 after Q_L (top wrote before P_L) and its
-// own rows after Q_L. WAR: top writes after R_L (bottom's c0..c5 of conv L done), bottom writes
-// after X_L (top's c12..c17 of conv L done at R_L); within a half every wave's reads precede the
-// barrier before its half's writes. Per SIMD the segments pair a wave's epilogue with its partner's
-// chunks (top's epilogue vs bottom's c6..c7, bottom's epilogue vs top's c8..c9, the stores vs
-// c8..c9 / c10..c11), so the matrix pipe has work throughout: 36 chunk-units a layer at ideal.
-// The B-fragment ring is primed after every barrier (no read crosses one); the weight ring runs on
-// across barriers and layers (read-only).
-constexpr int kPpThreads = 512;
-
-template <int N>
-struct LnHalfMap {
-  static constexpr int NN = N * N, H = N / 2, NH = H * N, NGH = (NH + 15) / 16, RS = ln_row(N);
-  int slot[2][NGH * 16];
-  constexpr LnHalfMap() : slot() {
-    for (int h = 0; h < 2; ++h) {
-      bool used[NH] = {};
-      for (int i = 0; i < NGH * 16; ++i) slot[h][i] = -1;
-      for (int g = 0; g < NGH; ++g)
-        for (int r = 0; r < 16; ++r)
-          for (int p = 0; p < NH; ++p) {
-            const int q = h * NH + p, sl = (q / N + 1) * RS + q % N + 1;
-            if (!used[p] && sl % 16 == r) {
-              used[p] = true;
-              slot[h][g * 16 + r] = sl;
-              break;
-            }
-          }
-      int p = 0;
-      for (int i = 0; i < NGH * 16; ++i) {
-        if (slot[h][i] >= 0) continue;
-        while (p < NH && used[p]) ++p;
-        if (p == NH) break;
-        used[p] = true;
-        const int q = h * NH + p;
-        slot[h][i] = (q / N + 1) * RS + q % N + 1;
-      }
-    }
-  }
-};
-template <int N>
-__device__ constexpr LnHalfMap<N> kLnHalfMap{};
-// LDS of k_leafnet_x3p<N>: the 18 planes of k_leafnet_x3 + wave maxima (2 parities x 8 + 8)
-__host__ __device__ constexpr int lnp_lds_bytes(int N) { return 18 * ln_plane(N) + 128; }
-static_assert(lnp_lds_bytes(20) <= 160 * 1024, "k_leafnet_x3p<20>: LDS");
-
-template <int C>
-using IC = std::integral_constant<int, C>;
-
-#if BK_LN_STAMP
-// diagnostic build: per wave, s_memtime before / after each of the first 15 tower barriers
-// (slots 2b, 2b + 1 of barrier b counted from P_0), slot 30 kernel start, 31 end (bk_lnp_stamps)
-__device__ unsigned long long g_lnp_stamps[256 * 8 * 32];
-#endif
-template <int N>
-__global__ __launch_bounds__(kPpThreads, 2) void k_leafnet_x3p(const float* __restrict__ obs,
-                                                              const h16x8* __restrict__ wstem,
-                                                              const float* __restrict__ sstem,
-                                                              const float* __restrict__ bstem,
-                                                              const h16x8* __restrict__ wt,
-                                                              const float* __restrict__ st,
-                                                              const float* __restrict__ bt,
-                                                              const float* __restrict__ bounds, int nlayers,
-                                                              LnHeads hd, float* __restrict__ xout) {
-  constexpr int NN = N * N, RS = ln_row(N), PL = ln_plane(N), NG = LnHalfMap<N>::NGH;
-  constexpr int PIX_IT = (NN + kPpThreads - 1) / kPpThreads;
-  constexpr int S = kLnPf + 1;  // B-fragment ring slots
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  unsigned char* act = lds;            // 16 planes [hi q | lo q][(N+2) x RS slots][16 B]
-  unsigned char* sin = lds + 16 * PL;  // 2 planes: the stem input hi, lo
-  float* red = reinterpret_cast<float*>(lds + 18 * PL);  // [2 parities][8 waves] maxima, [8] block max
-  const int tid = threadIdx.x, l = tid & 63, n = l & 15, ks = l >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
-  const int half = wave >> 2, cb = wave & 3;
-  const int oc = 16 * cb + 4 * ks;  // the lane's 4 output channels oc..oc+3 in the D fragments
-  const size_t b = blockIdx.x;
-
-  const float* ob = obs + b * kStemCinX3 * NN;
-  float xin[PIX_IT][kStemCinX3];
-#pragma unroll
-  for (int it = 0; it < PIX_IT; ++it) {
-    const int p = tid + it * kPpThreads;
-#pragma unroll
-    for (int c = 0; c < kStemCinX3; ++c) xin[it][c] = p < NN ? ob[c * NN + p] : 0.0f;
-  }
-  {  // the halo of all 18 planes (as k_leafnet_x3)
-    constexpr int kHaloCols = RS - N, kHalo = 2 * RS + N * kHaloCols;
-    for (int i = tid; i < 18 * kHalo; i += kPpThreads) {
-      const int plane = i / kHalo, k = i - plane * kHalo;
-      int row, col;
-      if (k < 2 * RS) {
-        row = k < RS ? 0 : N + 1;
-        col = k < RS ? k : k - RS;
-      } else {
-        const int h = k - 2 * RS, c = h % kHaloCols;
-        row = 1 + h / kHaloCols;
-        col = c == 0 ? 0 : N + c;
-      }
-      *reinterpret_cast<u32x4*>(lds + plane * PL + (row * RS + col) * 16) = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-
-  constexpr int kBias = (RS + 1) * 16;
-  int ab[NG];
-  unsigned valid = 0;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int sl = kLnHalfMap<N>.slot[half][16 * g + n];
-    ab[g] = (sl >= 0 ? sl : RS + 1) * 16 + ks * 4 * PL - kBias;
-    valid |= (sl >= 0 ? 1u : 0u) << g;
-  }
-  auto is_valid = [&](int g) { return ((NN / 2) % 16 == 0) || ((valid >> g) & 1u); };
-  auto slot_b = [&](int g) { return ab[g] - ks * 4 * PL + kBias; };
-
-  static_assert(18 % (kLnWpf + 1) == 0, "BK_LN_WPF: the ring must divide the 18 chunks of a layer");
-  constexpr int kLayerBlocks = 18 * 4 * 2;
-  const __amdgpu_buffer_rsrc_t wrs = ln_rsrc(wt, (unsigned)nlayers * kLayerBlocks * 1024u);
-  auto wload = [&](int layer, int c, int p) {
-    return __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                         wrs, l * 16, ((layer * kLayerBlocks + c * 8 + cb * 2 + p) * 64) * 16, 0));
-  };
-  h16x8 wq[kLnWpf + 1][2];
-#pragma unroll
-  for (int c = 0; c < kLnWpf; ++c) {
-    wq[c][0] = wload(0, c, 0);
-    wq[c][1] = wload(0, c, 1);
-  }
-
-  // ---- stem input: scaled by the board maximum, split (all 8 waves)
-  float max_obs;
-  {
-    float m = 0.0f;
-#pragma unroll
-    for (int it = 0; it < PIX_IT; ++it)
-#pragma unroll
-      for (int c = 0; c < kStemCinX3; ++c) m = fmaxf(m, fabsf(xin[it][c]));
-    m = wave_max_f(m);
-    if (l == 0) red[16 + wave] = m;
-    __syncthreads();  // also orders the halo zeroing before the writes below
-    max_obs = fmaxf(fmaxf(fmaxf(red[16], red[17]), fmaxf(red[18], red[19])),
-                    fmaxf(fmaxf(red[20], red[21]), fmaxf(red[22], red[23])));
-  }
-  int ex = scale_exp(max_obs);
-#pragma unroll
-  for (int it = 0; it < PIX_IT; ++it) {
-    const int p = tid + it * kPpThreads;
-    if (p < NN) {
-      unsigned h[4], o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) split2(ldexpf(xin[it][2 * q], ex), ldexpf(xin[it][2 * q + 1], ex), h[q], o[q]);
-      const u32x4 hi{h[0], h[1], h[2], h[3]}, lo{o[0], o[1], o[2], o[3]};
-      unsigned char* dst = sin + ((p / N + 1) * RS + p % N + 1) * 16;
-      *reinterpret_cast<u32x4*>(dst) = hi;
-      *reinterpret_cast<u32x4*>(dst + PL) = lo;
-    }
-  }
-  __syncthreads();  // the stem input is in LDS
-
-  f32x4 acc[NG];
-  // One K chunk over the half's NG groups with a B-fragment ring of S slots whose reads run kLnPf
-  // groups ahead within the segment [C0, C1): element i = (c - C0) NG + g sits in slot i % S.
-  auto mfma3 = [&](bool init, int g, h16x8 ah, h16x8 al, const h16x8 (&r)[2]) {
-    if (init)
-      asm volatile(
-          "v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\t"
-          "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
-          "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
-          : "=&v"(acc[g])
-          : "v"(ah), "v"(r[0]), "v"(al), "v"(r[1])
-          : "memory");
-    else
-      asm volatile(
-          "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
-          "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
-          "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
-          : "+v"(acc[g])
-          : "v"(ah), "v"(r[0]), "v"(al), "v"(r[1])
-          : "memory");
-  };
-  auto coff_of = [&](int c) {  // tower chunk c = (tap c/2, channel half c%2), as k_leafnet_x3
-    const int t = c >> 1;
-    return 2 * (c & 1) * PL + ((t / 3 - 1) * RS + (t % 3 - 1)) * 16 + kBias;
-  };
-  // tower chunks [C0, C1) of conv `layer` (weights: chunk c's A fragments in ring slot c % (Wpf+1),
-  // the loads kLnWpf chunks ahead, on into the next conv)
-  auto seg = [&](auto c0, auto c1, int layer) {
-    constexpr int C0 = decltype(c0)::value, C1 = decltype(c1)::value;
-    const bool more = layer + 1 < nlayers;
-    h16x8 rb[S][2];
-#pragma unroll
-    for (int g = 0; g < kLnPf; ++g) ln_load<PL>(rb[g % S], act, ab[g], coff_of(C0));
-#pragma unroll
-    for (int c = C0; c < C1; ++c) {
-      const int cn = c + kLnWpf, sn = cn % (kLnWpf + 1);
-      if (cn < 18) {
-        wq[sn][0] = wload(layer, cn, 0);
-        wq[sn][1] = wload(layer, cn, 1);
-      } else {
-        const int nl = more ? layer + 1 : layer;
-        wq[sn][0] = wload(nl, cn - 18, 0);
-        wq[sn][1] = wload(nl, cn - 18, 1);
-      }
-      const h16x8* w = wq[c % (kLnWpf + 1)];
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const int i = (c - C0) * NG + g, ip = i + kLnPf;
-        if (ip < (C1 - C0) * NG) ln_load<PL>(rb[ip % S], act, ab[ip % NG], coff_of(C0 + ip / NG));
-        mfma3(c == 0, g, w[0], w[1], rb[i % S]);
-      }
-    }
-  };
-  auto drain = [&]() {
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-    for (int g = 0; g < NG; ++g) asm volatile("" : "+v"(acc[g]));
-  };
-  // the stem conv (3 chunks over the stem grid), as k_leafnet_x3
-  auto stem = [&]() {
-    // the stem's weights (3 chunks): loaded here, not in the prologue (the bottom half runs its
-    // stem a segment later: nothing of it stays live across the top half's first chunks)
-    h16x8 wsa[3][2];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      wsa[j][0] = wstem[((j * 4 + cb) * 2) * 64 + l];
-      wsa[j][1] = wstem[((j * 4 + cb) * 2 + 1) * 64 + l];
-    }
-    auto toff = [&](int j) {
-      const int t = 4 * j + ks < 9 ? 4 * j + ks : 8;
-      return ((t / 3 - 1) * RS + (t % 3 - 1)) * 16 + kBias - ks * 4 * PL;
-    };
-    h16x8 rb[S][2];
-#pragma unroll
-    for (int g = 0; g < kLnPf; ++g) ln_load<PL>(rb[g % S], sin, ab[g], toff(0));
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const int i = j * NG + g, ip = i + kLnPf;
-        if (ip < 3 * NG) ln_load<PL>(rb[ip % S], sin, ab[ip % NG], toff(ip / NG));
-        mfma3(j == 0, g, wsa[j][0], wsa[j][1], rb[i % S]);
-      }
-    }
-  };
-
-  // epilogue of a conv (as k_leafnet_x3's): y = acc * s + bias (+ x0) (ReLU); OUT: scaled by
-  // 2^ex_out and split into acc; returns the lane's max |y| (unscaled)
-  auto epilogue = [&](f32x4 sv, f32x4 bv, bool relu, bool residual, const f32x4 (&x0)[NG], bool out, int ex_out) {
-    const int k = out ? ex_out : 0;
-    const f32x2 s01{ldexpf(sv.x, k - ex), ldexpf(sv.y, k - ex)}, s23{ldexpf(sv.z, k - ex), ldexpf(sv.w, k - ex)};
-    const f32x2 b01{ldexpf(bv.x, k), ldexpf(bv.y, k)}, b23{ldexpf(bv.z, k), ldexpf(bv.w, k)};
-    const int floor = relu ? 0 : (int)0x80000000u;
-    float mx = 0.0f;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      f32x2 y01 = pk_fma(f32x2{acc[g][0], acc[g][1]}, s01, b01);
-      f32x2 y23 = pk_fma(f32x2{acc[g][2], acc[g][3]}, s23, b23);
-      if (residual) {
-        y01 = pk_add(y01, f32x2{x0[g][0], x0[g][1]});
-        y23 = pk_add(y23, f32x2{x0[g][2], x0[g][3]});
-      }
-      y01 = f32x2{max_bits(y01.x, floor), max_bits(y01.y, floor)};
-      y23 = f32x2{max_bits(y23.x, floor), max_bits(y23.y, floor)};
-      if (is_valid(g)) mx = max3_abs(max3_abs(mx, y01.x, y01.y), y23.x, y23.y);
-      if (out) {
-        unsigned h0, h1, l0, l1;
-        split2(y01.x, y01.y, h0, l0);
-        split2(y23.x, y23.y, h1, l1);
-        acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
-                       __builtin_bit_cast(float, l1)};
-      } else {
-        acc[g] = f32x4{y01.x, y01.y, y23.x, y23.y};
-      }
-    }
-    return ldexpf(mx, -k);
-  };
-  // the packed halves in acc -> the activation grid (two 8-B stores per lane and group)
-  auto write_act = [&]() {
-    const int o = 2 * cb + (ks >> 1);
-    unsigned char* base = act + ((o & 3) * 4 + (o >> 2) * 2) * PL + (ks & 1) * 8;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);  // {hi 01, hi 23, lo 01, lo 23}
-      if (is_valid(g)) {
-        *reinterpret_cast<u32x2*>(base + slot_b(g)) = u32x2{w.x, w.y};
-        *reinterpret_cast<u32x2*>(base + slot_b(g) + PL) = u32x2{w.z, w.w};
-      }
-    }
-  };
-  auto post_max = [&](float mx, int par) {
-    mx = wave_max_f(mx);
-    if (l == 0) red[8 * par + wave] = mx;
-  };
-  auto board_max = [&](int par) {
-    const float* r = red + 8 * par;
-    return fmaxf(fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3])), fmaxf(fmaxf(r[4], r[5]), fmaxf(r[6], r[7])));
-  };
-
-  f32x4 x0[NG];
-  // the stem's epilogue: x0 kept unscaled (AGPRs) for the tower's final residual, the split input
-  // of conv 0 in acc; the max posted for conv 0's output bound
-  auto stem_epi = [&]() {
-    const f32x4 s_stem = *reinterpret_cast<const f32x4*>(sstem + oc);
-    const f32x4 b_stem = *reinterpret_cast<const f32x4*>(bstem + oc);
-    const int ex_out = scale_exp(bounds[0] * max_obs + bounds[1]);
-#pragma unroll
-    for (int g = 0; g < NG; ++g) x0[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float mx = epilogue(s_stem, b_stem, true, false, x0, false, 0);
-#pragma unroll
-    for (int g = 0; g < NG; ++g) x0[g] = acc[g];
-    const float up = ldexpf(1.0f, ex_out);
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      unsigned h0, h1, l0, l1;
-      split2(x0[g][0] * up, x0[g][1] * up, h0, l0);
-      split2(x0[g][2] * up, x0[g][3] * up, h1, l1);
-      acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
-                     __builtin_bit_cast(float, l1)};
-    }
-    post_max(mx, 0);
-    ex = ex_out;
-  };
-  // a tower conv's epilogue (not the last): the output scale from the bound on |y| over the board
-  // maximum of its input (parity layer & 1, posted by both halves' previous epilogues)
-  auto conv_epi = [&](int layer) {
-    const f32x4 sv = *reinterpret_cast<const f32x4*>(st + layer * 64 + oc);
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + layer * 64 + oc);
-    const float max_in = board_max(layer & 1);
-    const int ex_out = scale_exp(bounds[2 * (layer + 1)] * max_in + bounds[2 * (layer + 1) + 1]);
-    const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
-    post_max(mx, (layer + 1) & 1);
-    ex = ex_out;
-  };
-  auto last_epi = [&](int layer) {
-    const f32x4 sv = *reinterpret_cast<const f32x4*>(st + layer * 64 + oc);
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + layer * 64 + oc);
-    epilogue(sv, bv, true, true, x0, false, 0);
-  };
-
-  int nbar = 0;  // tower barriers passed (diagnostic stamps)
-  auto bar = [&]() {
-#if BK_LN_STAMP
-    if (l == 0 && blockIdx.x < 256 && nbar < 15) g_lnp_stamps[(blockIdx.x * 8 + wave) * 32 + 2 * nbar] = __builtin_amdgcn_s_memtime();
-#endif
-    __syncthreads();
-#if BK_LN_STAMP
-    if (l == 0 && blockIdx.x < 256 && nbar < 15) g_lnp_stamps[(blockIdx.x * 8 + wave) * 32 + 2 * nbar + 1] = __builtin_amdgcn_s_memtime();
-#endif
-    ++nbar;
-  };
-#if BK_LN_STAMP
-  if (l == 0 && blockIdx.x < 256) g_lnp_stamps[(blockIdx.x * 8 + wave) * 32 + 30] = __builtin_amdgcn_s_memtime();
-#endif
-  if (half == 0) {  // top half: leads by about half a layer
-    stem();
-    drain();
-    stem_epi();
-    write_act();
-    bar();  // P_0
-    for (int layer = 0; layer < nlayers; ++layer) {
-      seg(IC<0>{}, IC<10>{}, layer);
-      bar();  // X_{L-1}
-      seg(IC<10>{}, IC<12>{}, layer);
-      bar();  // Q_L
-      seg(IC<12>{}, IC<18>{}, layer);
-      drain();
-      if (layer + 1 == nlayers) {
-        last_epi(layer);
-        bar();  // R
-        bar();  // P
-        bar();  // X: the bottom half's last reads are done
-        break;
-      }
-      conv_epi(layer);
-      bar();  // R_L
-      write_act();
-      bar();  // P_{L+1}
-    }
-  } else {  // bottom half
-    bar();  // P_0
-    stem();
-    drain();
-    stem_epi();
-    bar();  // X_{-1}
-    write_act();
-    bar();  // Q_0
-    for (int layer = 0; layer < nlayers; ++layer) {
-      seg(IC<0>{}, IC<8>{}, layer);
-      bar();  // R_L
-      seg(IC<8>{}, IC<10>{}, layer);
-      bar();  // P_{L+1}
-      seg(IC<10>{}, IC<18>{}, layer);
-      drain();
-      if (layer + 1 == nlayers) {
-        last_epi(layer);
-        bar();  // X
-        break;
-      }
-      conv_epi(layer);
-      bar();  // X_L
-      write_act();
-      bar();  // Q_{L+1}
-    }
-  }
-
-  // ---- outputs: the tower output (optional) and the heads (blokus_nnet.py:146-150, BN folded);
-  // every wave's reads of the grid are done (the last barrier above)
-  if (xout) {
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-      if (is_valid(g))
-        *reinterpret_cast<f32x4*>(xout + (b * NN + ln_pixel<N>(slot_b(g) / 16)) * 64 + oc) = acc[g];
-  }
-  float* hp = reinterpret_cast<float*>(act);  // [NN][4 channel blocks][3]
-  {
-    const f32x4 wp0 = *reinterpret_cast<const f32x4*>(hd.wp + oc);
-    const f32x4 wp1 = *reinterpret_cast<const f32x4*>(hd.wp + 64 + oc);
-    const f32x4 wvv = *reinterpret_cast<const f32x4*>(hd.wv + oc);
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const f32x4 y = acc[g];
-      float d[3];
-      const f32x4* w[3] = {&wp0, &wp1, &wvv};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float a = y.x * (*w[k]).x + y.y * (*w[k]).y + y.z * (*w[k]).z + y.w * (*w[k]).w;
-        const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
-        const float a16 = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
-        const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a16), __float_as_uint(a16), false, false);
-        d[k] = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
-      }
-      if (ks == 0 && is_valid(g)) {
-        float* dst = hp + (ln_pixel<N>(slot_b(g) / 16) * 4 + cb) * 3;
-        dst[0] = d[0];
-        dst[1] = d[1];
-        dst[2] = d[2];
-      }
-    }
-  }
-  __syncthreads();
-  float* vfeat = hp + NN * 12;
-  float* part = vfeat + NN;
-  for (int i = tid; i < NN; i += kPpThreads) {
-    const float* q = hp + i * 12;
-    const float p0 = ((q[0] + q[3]) + q[6]) + q[9], p1 = ((q[1] + q[4]) + q[7]) + q[10],
-                pv = ((q[2] + q[5]) + q[8]) + q[11];
-    hd.pf[b * 2 * NN + i] = fmaxf(p0 + hd.bp[0], 0.0f);
-    hd.pf[b * 2 * NN + NN + i] = fmaxf(p1 + hd.bp[1], 0.0f);
-    vfeat[i] = fmaxf(pv + hd.bv[0], 0.0f);
-  }
-  __syncthreads();
-  if (wave < 4) {  // the value MLP exactly as k_leafnet_x3 (4 waves, quarters of W1's inputs)
-    constexpr int Q = NN / 4;
-    static_assert(NN % 4 == 0, "k_leafnet_x3p: quarters of the value-MLP inputs");
-    const int q0 = Q * wave;
-    float w[Q];
-#pragma unroll
-    for (int k = 0; k < Q; ++k) w[k] = hd.w1t[(size_t)(q0 + k) * 64 + l];
-    float a0 = 0.f, a1 = 0.f;
-    int k = 0;
-#pragma unroll
-    for (; k + 10 <= Q; k += 10) {
-#pragma unroll
-      for (int u = 0; u < 10; u += 2) {
-        a0 += w[k + u] * vfeat[q0 + k + u];
-        a1 += w[k + u + 1] * vfeat[q0 + k + u + 1];
-      }
-    }
-#pragma unroll
-    for (; k < Q; ++k) a0 += w[k] * vfeat[q0 + k];
-    part[wave * 64 + l] = a0 + a1;
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const float h = fmaxf(((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) + hd.b1[l], 0.0f);
-    for (int q = 0; q < hd.P; ++q) {
-      const float sum = wave_sum_f(hd.w2[q * 64 + l] * h);
-      if (l == 0) hd.v[b * hd.P + q] = tanhf(sum + hd.b2[q]);
-    }
-  }
-#if BK_LN_STAMP
-  if (l == 0 && blockIdx.x < 256) g_lnp_stamps[(blockIdx.x * 8 + wave) * 32 + 31] = __builtin_amdgcn_s_memtime();
-#endif
-}
-
 }  // namespace
 }  // namespace bk
 
@@ -957,9 +452,6 @@ int bk_leafnet_x3_weight_bytes(int cin) {
 int bk_leafnet_x3_supported(int N) { return N == 14 || N == 20; }
 
 #if BK_LN_STAMP
-int bk_lnp_stamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lnp_stamps), sizeof(g_lnp_stamps)) == hipSuccess ? 0 : -1;
-}
 int bk_ln_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ln_stamps), sizeof(g_ln_stamps)) == hipSuccess ? 0 : -1;
 }
@@ -985,24 +477,13 @@ int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, co
              "bk_leafnet_x3: 16-byte aligned buffers");
   if (B == 0) return BK_OK;
   {
-    const void* fns[4] = {(const void*)k_leafnet_x3<14>, (const void*)k_leafnet_x3<20>,
-                          (const void*)k_leafnet_x3p<14>, (const void*)k_leafnet_x3p<20>};
-    if (set_max_dynamic_lds(fns, 4, lnp_lds_bytes(20)) != BK_OK) return BK_EHIP;
+    const void* fns[2] = {(const void*)k_leafnet_x3<14>, (const void*)k_leafnet_x3<20>};
+    if (set_max_dynamic_lds(fns, 2, ln_lds_bytes(20)) != BK_OK) return BK_EHIP;
   }
   const LnHeads h{wp, bp, wv, bv, w1t, b1, w2, b2, P, pf, vout};
   hipStream_t s = (hipStream_t)stream;
   const h16x8* ws = reinterpret_cast<const h16x8*>(wstem);
   const h16x8* wt = reinterpret_cast<const h16x8*>(wtower);
-  const char* pp = getenv("BK_LN_PP");  // A/B: the 8-wave skewed form k_leafnet_x3p (read per call)
-  if (pp && atoi(pp)) {
-    if (N == 20)
-      hipLaunchKernelGGL(k_leafnet_x3p<20>, dim3(B), dim3(kPpThreads), lnp_lds_bytes(20), s, obs, ws, sstem, bstem,
-                         wt, stower, btower, bounds, nlayers, h, out);
-    else
-      hipLaunchKernelGGL(k_leafnet_x3p<14>, dim3(B), dim3(kPpThreads), lnp_lds_bytes(14), s, obs, ws, sstem, bstem,
-                         wt, stower, btower, bounds, nlayers, h, out);
-    return launch_check("k_leafnet_x3p");
-  }
   if (N == 20)
     hipLaunchKernelGGL(k_leafnet_x3<20>, dim3(B), dim3(kLnThreads), ln_lds_bytes(20), s, obs, ws, sstem, bstem, wt,
                        stower, btower, bounds, nlayers, h, out);

@@ -151,28 +151,29 @@ __global__ __launch_bounds__(64) void k_vec_step(DevPreset dp, uint32_t* states,
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_vec_step7: the same step for the 7x7 presets (config 5), EIGHT lanes per env instead of a
-// wave. A 7x7 colour is one u64 bitboard with rows at stride 8 (bit 8 r + c; column 7 is a guard
+// k_vec_step7: the same step for the 7x7 presets (config 5), G = 16 (or 8) lanes per env instead
+// of a wave. A 7x7 colour is one u64 bitboard with rows at stride 8 (bit 8 r + c; column 7 is a guard
 // that absorbs the +-1 column shifts), so a colour's forbidden / anchor cells are a handful of
 // 64-bit shifts and the legal origins of a fixed orientation are
 //   L_o = VALID_o & ~OR_k (F >> off_k) & OR_k (A >> off_k)      (off_k = 8 dr_k + dc_k)
 // (compute_fa + eval_item of common.h on whole boards). The orientations are dealt round robin
-// to the 8 lanes of an env (orientation 8 i + j to lane j: 4 per lane for the 919-id preset, 12
-// for the 2522-id one), each lane holding its orientations' cells / valid origins / id base in
+// to the G lanes of an env (orientation G i + j to lane j: 2 per lane for the 919-id preset, 6
+// for the 2522-id one at G = 16), each lane holding its orientations' cells / valid origins / id base in
 // registers. Counting, the k-th legal id (ascending id = ascending orientation, then origin bit
 // r*8 + c, as the bitmask order), hash updates and the legal-move mask are per-lane work met by
-// 3-step DPP butterflies inside the octet; obs and mask are staged in LDS and leave as coalesced
+// 3- or 4-step DPP butterflies inside the env's lanes; obs and mask are staged in LDS and leave as coalesced
 // rows. Only the state words a 2-colour 7x7 game uses are read and written (occupancy rows 0..6
 // of colours 0 and 1, pieces, hash, to-move, ply, flags); the rest of the 384-B state stays as
 // bk_vec_reset wrote it (zero). Bitwise the trajectories of k_vec_step (tests/test_vecenv_gpu.py).
 constexpr uint64_t kBoard7 = 0x007F7F7F7F7F7F7Full;  // rows 0..6 x columns 0..6 at stride 8
-constexpr int kVecThreads = 256, kVecEnvsPerBlock = kVecThreads / 8;
+constexpr int kVecThreads = 256;
 
-template <int MC>
+template <int MC, int G>
 struct Vec7 {
   static constexpr int NO = MC == 4 ? 28 : 91;     // fixed orientations of the <= MC-cell pieces
   static constexpr int NP = MC == 4 ? 9 : 21;      // pieces
-  static constexpr int NL = (NO + 7) / 8;          // orientations per lane
+  static constexpr int NL = (NO + G - 1) / G;      // orientations per lane (G lanes per env)
+  static constexpr int EPB = kVecThreads / G;      // envs per workgroup
   static constexpr int A = MC == 4 ? 919 : 2522;   // action ids
   static constexpr int W64 = (A + 63) / 64, W32 = (A + 31) / 32;
 };
@@ -184,10 +185,10 @@ struct Or7 {
 };
 template <int MC>
 struct Or7Table {
-  Or7 o[Vec7<MC>::NO];
+  Or7 o[Vec7<MC, 8>::NO];
   constexpr Or7Table() : o() {
     int id = 0;
-    for (int k = 0; k < Vec7<MC>::NO; ++k) {
+    for (int k = 0; k < Vec7<MC, 8>::NO; ++k) {
       const OrientC& q = kOrient[k];
       uint32_t offs = 0;
       for (int i = 0; i < 5; ++i) offs |= (uint32_t)(q.dr[i] * 8 + q.dc[i]) << (6 * i);
@@ -203,45 +204,56 @@ struct Or7Table {
 template <int MC>
 __device__ constexpr Or7Table<MC> kOr7{};
 
-// octet (8-lane) collectives on DPP: quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror
+// collectives over the G (8 or 16) lanes of an env, on DPP: quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror (8 lanes), then row_mirror (16 lanes)
 template <int CTRL>
 __device__ __forceinline__ uint32_t dppu(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
-__device__ __forceinline__ int oct_sum(int x) {
+template <int G>
+__device__ __forceinline__ int grp_sum(int x) {
   x += (int)dppu<0xB1>((uint32_t)x);
   x += (int)dppu<0x4E>((uint32_t)x);
   x += (int)dppu<0x141>((uint32_t)x);
+  if (G == 16) x += (int)dppu<0x140>((uint32_t)x);
   return x;
 }
-__device__ __forceinline__ uint64_t oct_or64(uint64_t x) {
+template <int G, typename OP>
+__device__ __forceinline__ uint64_t grp_red64(uint64_t x, OP op) {
   uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  lo |= dppu<0xB1>(lo);
-  hi |= dppu<0xB1>(hi);
-  lo |= dppu<0x4E>(lo);
-  hi |= dppu<0x4E>(hi);
-  lo |= dppu<0x141>(lo);
-  hi |= dppu<0x141>(hi);
+  lo = op(lo, dppu<0xB1>(lo));
+  hi = op(hi, dppu<0xB1>(hi));
+  lo = op(lo, dppu<0x4E>(lo));
+  hi = op(hi, dppu<0x4E>(hi));
+  lo = op(lo, dppu<0x141>(lo));
+  hi = op(hi, dppu<0x141>(hi));
+  if (G == 16) {
+    lo = op(lo, dppu<0x140>(lo));
+    hi = op(hi, dppu<0x140>(hi));
+  }
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t oct_xor64(uint64_t x) {
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  lo ^= dppu<0xB1>(lo);
-  hi ^= dppu<0xB1>(hi);
-  lo ^= dppu<0x4E>(lo);
-  hi ^= dppu<0x4E>(hi);
-  lo ^= dppu<0x141>(lo);
-  hi ^= dppu<0x141>(hi);
-  return ((uint64_t)hi << 32) | lo;
+template <int G>
+__device__ __forceinline__ uint64_t grp_or64(uint64_t x) {
+  return grp_red64<G>(x, [](uint32_t a, uint32_t b) { return a | b; });
 }
-// inclusive prefix sum over lanes 0..j of the octet (row_shr 1, 2, 4 inside each 8-lane segment)
-__device__ __forceinline__ int oct_incl(int x, int j) {
+template <int G>
+__device__ __forceinline__ uint64_t grp_xor64(uint64_t x) {
+  return grp_red64<G>(x, [](uint32_t a, uint32_t b) { return a ^ b; });
+}
+// inclusive prefix sum over lanes 0..j of the env's group (row_shr 1, 2, 4 (, 8) inside it)
+template <int G>
+__device__ __forceinline__ int grp_incl(int x, int j) {
   int t = (int)dppu<0x111>((uint32_t)x);
   if (j >= 1) x += t;
   t = (int)dppu<0x112>((uint32_t)x);
   if (j >= 2) x += t;
   t = (int)dppu<0x114>((uint32_t)x);
   if (j >= 4) x += t;
+  if (G == 16) {
+    t = (int)dppu<0x118>((uint32_t)x);
+    if (j >= 8) x += t;
+  }
   return x;
 }
 // bit index of the k-th (0-based) set bit of x (k < popcount(x)): binary search on popcounts
@@ -262,27 +274,44 @@ __device__ __forceinline__ int kth_bit64(uint64_t x, int k) {
   return pos;
 }
 
-template <int MC>
+#ifdef BK_VEC_STAMP
+// diagnostic build only: per wave (lane 0), s_memtime at the phases of k_vec_step7 (bk_vec_stamps)
+__device__ unsigned long long g_vec_stamps[4096][8];
+#define VSTAMP(i)                                                                   \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0) {                                                  \
+      const int w_ = blockIdx.x * (kVecThreads / 64) + (threadIdx.x >> 6);          \
+      if (w_ < 4096) g_vec_stamps[w_][i] = __builtin_amdgcn_s_memtime();            \
+    }                                                                               \
+  } while (0)
+#else
+#define VSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
+template <int MC, int G>
 __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uint64_t* rng,
                                                           const int32_t* __restrict__ actions, int E,
                                                           uint8_t* __restrict__ obs, uint64_t* __restrict__ mask,
                                                           float* __restrict__ reward, int32_t* __restrict__ done) {
-  using V = Vec7<MC>;
-  constexpr int NL = V::NL;
+  using V = Vec7<MC, G>;
+  constexpr int NL = V::NL, kVecEnvsPerBlock = V::EPB;
   __shared__ uint32_t m32[kVecEnvsPerBlock][V::W32 + 1];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kVecEnvsPerBlock * 49 + 16];
-  const int tid = threadIdx.x, j = tid & 7, le = tid >> 3;
+  const int tid = threadIdx.x, j = tid & (G - 1), le = tid / G;
   const int e0 = blockIdx.x * kVecEnvsPerBlock;
+  VSTAMP(0);
   const int e = e0 + le;
   const bool live = e < E;
-  const int es = live ? e : E - 1;  // a spare octet mirrors the last env and stores nothing
+  const int es = live ? e : E - 1;  // a spare lane group mirrors the last env and stores nothing
 
   // this lane's orientations (8 i + j): cells, valid origins, meta
   uint32_t offs[NL], meta[NL];
   uint64_t valid[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
-    const int k = 8 * i + j;
+    const int k = G * i + j;
     const Or7 q = kOr7<MC>.o[k < V::NO ? k : 0];
     offs[i] = q.offs;
     meta[i] = q.meta;
@@ -329,11 +358,11 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
       L[i] = have ? (valid[i] & ~fo & ao) : 0ull;
       cnt += __popcll(L[i]);
     }
-    lastK = oct_sum(cnt);
+    lastK = grp_sum<G>(cnt);
     return lastK;
   };
   // the k-th legal id in ascending order -> (id, the orientation's offs, meta, origin bit), the
-  // same in every lane of the octet
+  // same in every lane of the env's group
   struct Pick {
     int id;
     uint32_t offs, meta;
@@ -346,7 +375,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = __popcll(L[i]);
-      const int incl = oct_incl(c, j), tot = oct_sum(c);
+      const int incl = grp_incl<G>(c, j), tot = grp_sum<G>(c);
       const int kk = k - before - (incl - c);
       if (kk >= 0 && kk < c) {
         const int pos = kth_bit64(L[i], kk);
@@ -358,8 +387,8 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
       }
       before += tot;
     }
-    sel = oct_or64(sel);
-    const uint64_t om = oct_or64(((uint64_t)sm << 32) | so);
+    sel = grp_or64<G>(sel);
+    const uint64_t om = grp_or64<G>(((uint64_t)sm << 32) | so);
     return Pick{(int)(sel & 0xFFFFu), (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 16) & 63u)};
   };
   // decode a given id -> the same Pick; id -1 when it is out of range or not a legal origin of the
@@ -380,8 +409,8 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
         }
       }
     }
-    sel = oct_or64(sel);
-    const uint64_t om = oct_or64(((uint64_t)sm << 32) | so);
+    sel = grp_or64<G>(sel);
+    const uint64_t om = grp_or64<G>(((uint64_t)sm << 32) | so);
     return Pick{(sel >> 63) ? (int)(sel & 0xFFFFu) : -1, (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 16) & 63u)};
   };
   // place pick p for colour q: cells, pieces, ply, the board hash (rows r.. r+h-1, one lane each)
@@ -397,7 +426,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
       const uint32_t o = (uint32_t)(before >> (8 * row)) & 0x7Fu, nw = (uint32_t)(after >> (8 * row)) & 0x7Fu;
       hx = (o ? row_key(q, row, o) : 0ull) ^ row_key(q, row, nw);
     }
-    hash ^= oct_xor64(hx);
+    hash ^= grp_xor64<G>(hx);
     occ[q] = after;
     pieces[q] &= ~(1u << ((p.meta >> 12) & 31u));
     ply += 1u;
@@ -430,6 +459,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   int fin = 0;
   const int a = actions ? actions[es] : -1;
   const int K0 = legal(0);  // the agent (colour 0) is to move at every step start
+  VSTAMP(1);
   // the agent's move: the given id if it is legal, else (a < 0) a uniformly random legal one
   Pick pk = a >= 0 ? decode(a) : (K0 > 0 ? kth((int)rng_index(&st, K0)) : Pick{-1, 0u, 0u, 0});
   if (pk.id < 0) {  // an illegal agent action (or no legal move) ends the episode as a loss
@@ -438,6 +468,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   } else {
     place(0, pk);
     advance(0);
+    VSTAMP(2);
     // the built-in random opponent moves while it is colour 1's turn (advance left its origins in L)
     while (!(flags & kFlagOver) && to_move == 1) {
       const Pick pb = kth((int)rng_index(&st, lastK));
@@ -450,6 +481,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
       fin = 1;
     }
   }
+  VSTAMP(3);
   if (fin) {  // auto-reset (gymnasium vector-env semantics): init_state_lds's words
     occ[0] = occ[1] = 0ull;
     pieces[0] = pieces[1] = (1u << V::NP) - 1u;
@@ -460,8 +492,9 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     last_q = -1;
   }
   if (last_q != 0) legal(0);  // the agent's legal origins for its mask
+  VSTAMP(4);
 
-  // ---- outputs: the state words, rng, reward, done (lane 0 of the octet); obs and mask via LDS
+  // ---- outputs: the state words, rng, reward, done (lanes 0..3 of the env's group); obs and mask via LDS
   for (int w = tid; w < kVecEnvsPerBlock * (V::W32 + 1); w += kVecThreads) (&m32[0][0])[w] = 0u;
   __syncthreads();
   if (live) {
@@ -496,19 +529,21 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     // mask: each legal origin row of the lane's orientations ORed into the env's LDS words
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      uint64_t x = L[i];
       const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u);
-      while (x) {
-        const int r = (__ffsll((unsigned long long)x) - 1) >> 3;
-        const uint32_t bits = (uint32_t)(x >> (8 * r)) & 0x7Fu;
-        x &= ~(0xFFull << (8 * r));
-        const int pos = base + r * W, w = pos >> 5, sh = pos & 31;
-        atomicOr(&m32[le][w], bits << sh);
-        if (sh + W > 32) atomicOr(&m32[le][w + 1], bits >> (32 - sh));
+#pragma unroll
+      for (int r = 0; r < 7; ++r) {
+        const uint32_t bits = (uint32_t)(L[i] >> (8 * r)) & 0x7Fu;
+        if (bits) {
+          const int pos = base + r * W, w = pos >> 5, sh = pos & 31;
+          atomicOr(&m32[le][w], bits << sh);
+          if (sh + W > 32) atomicOr(&m32[le][w + 1], bits >> (32 - sh));
+        }
       }
     }
   }
+  VSTAMP(5);
   __syncthreads();
+  VSTAMP(6);
   // the block's envs are contiguous: obs rows as dwords, mask rows as u64 (coalesced)
   const int nenv = min(kVecEnvsPerBlock, E - e0);
   {
@@ -524,6 +559,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     const int le2 = i / V::W64, w = i - le2 * V::W64;
     mask[(size_t)(e0 + le2) * V::W64 + w] = (uint64_t)m32[le2][2 * w] | ((uint64_t)m32[le2][2 * w + 1] << 32);
   }
+  VSTAMP(7);
 }
 
 }  // namespace
@@ -536,6 +572,12 @@ static size_t vec_lds(const DevPreset& dp) {
 }
 
 extern "C" {
+
+#ifdef BK_VEC_STAMP
+int bk_vec_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vec_stamps), sizeof(g_vec_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int bk_vec_reset(bk_ctx* c, void* states, uint64_t* rng, const uint64_t* seeds, int E, uint8_t* obs,
                  uint64_t* mask, void* stream) {
@@ -556,13 +598,19 @@ int bk_vec_step(bk_ctx* c, void* states, uint64_t* rng, const int32_t* actions, 
   if (E == 0) return BK_OK;
   const char* g = getenv("BK_VEC_WAVE");  // A/B: the one-wave-per-env kernel on 7x7 too
   if (c->dp.N == 7 && (c->dp.num_pieces == 9 || c->dp.num_pieces == 21) && !(g && atoi(g))) {
-    const dim3 grid((E + kVecEnvsPerBlock - 1) / kVecEnvsPerBlock);
-    if (c->dp.num_pieces == 9)
-      hipLaunchKernelGGL(k_vec_step7<4>, grid, dim3(kVecThreads), 0, (hipStream_t)stream, (uint32_t*)states, rng,
-                         actions, E, obs, mask, reward, done);
+    const char* gl = getenv("BK_VEC_LANES");  // A/B: lanes per env (8 or 16)
+    const int G = gl && atoi(gl) == 8 ? 8 : 16;
+    const dim3 grid((E + kVecThreads / G - 1) / (kVecThreads / G));
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t* sp = (uint32_t*)states;
+    if (c->dp.num_pieces == 9 && G == 16)
+      hipLaunchKernelGGL((k_vec_step7<4, 16>), grid, dim3(kVecThreads), 0, st, sp, rng, actions, E, obs, mask, reward, done);
+    else if (c->dp.num_pieces == 9)
+      hipLaunchKernelGGL((k_vec_step7<4, 8>), grid, dim3(kVecThreads), 0, st, sp, rng, actions, E, obs, mask, reward, done);
+    else if (G == 16)
+      hipLaunchKernelGGL((k_vec_step7<5, 16>), grid, dim3(kVecThreads), 0, st, sp, rng, actions, E, obs, mask, reward, done);
     else
-      hipLaunchKernelGGL(k_vec_step7<5>, grid, dim3(kVecThreads), 0, (hipStream_t)stream, (uint32_t*)states, rng,
-                         actions, E, obs, mask, reward, done);
+      hipLaunchKernelGGL((k_vec_step7<5, 8>), grid, dim3(kVecThreads), 0, st, sp, rng, actions, E, obs, mask, reward, done);
     return launch_check("k_vec_step7");
   }
   hipLaunchKernelGGL(k_vec_step, dim3(E), dim3(kWave), vec_lds(c->dp), (hipStream_t)stream, c->dp,

@@ -52,6 +52,14 @@ class BlokusVectorEnv:
         term = self.done.bool()
         return self.obs, self.reward, term, torch.zeros_like(term), {}
 
+    def step_raw(self, actions: torch.Tensor | None = None):
+        """The env step alone (one bk_vec_step launch, no result tensors built): obs, mask_words,
+        reward and done are updated in place. Capturable in a HIP graph."""
+        act = None if actions is None else actions
+        _check(self.eng.lib.bk_vec_step(self.eng.h, _ptr(self.states), _ptr(self.rng), _ptr(act), self.num_envs,
+                                        _ptr(self.obs), _ptr(self.mask_words), _ptr(self.reward), _ptr(self.done),
+                                        self._s()))
+
     def valid_mask(self) -> torch.Tensor:
         """[E, A] bool: the agent's legal ids (the reference's ai_possible_indexes as a mask)."""
         return self.eng.unpack_mask(self.mask_words)
