@@ -342,21 +342,6 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
                          (const uint4*)c->d_pack, mask_words, counts);
       return launch_check("k_legal_mask_staged");
     }
-    case 41:    // piece lists over the active rows (legal_rows.h), 8 boards per workgroup
-    case 42:    // 12 boards
-    case 43: {  // 4 boards
-      const int nbw = c->legal_wpb == 42 ? 12 : c->legal_wpb == 43 ? 4 : 8;
-      if (nbw * c->dp.N > 256) { BK_LEGAL_LAUNCH(1, 0); break; }
-      const dim3 g((B + nbw - 1) / nbw);
-      const size_t bytes = sizeof(uint32_t) * nbw * (size_t)c->dp.W32pad;
-      if (nbw == 12)
-        hipLaunchKernelGGL(k_legal_mask_pieces<12>, g, dim3(256), bytes, st, c->dp, sp, players, B, mask_words, counts);
-      else if (nbw == 4)
-        hipLaunchKernelGGL(k_legal_mask_pieces<4>, g, dim3(256), bytes, st, c->dp, sp, players, B, mask_words, counts);
-      else
-        hipLaunchKernelGGL(k_legal_mask_pieces<8>, g, dim3(256), bytes, st, c->dp, sp, players, B, mask_words, counts);
-      return launch_check("k_legal_mask_pieces");
-    }
     case 11: BK_LEGAL_LAUNCH(1, 1); break;  // even/odd origin rows in separate LDS atomics: 15.1 vs 12.1 us
     default: BK_LEGAL_LAUNCH(1, 0); break;  // 1: one wave per group of 3 boards (the default)
   }

@@ -544,196 +544,4 @@ __global__ __launch_bounds__(64) void k_legal_mask_staged(DevPreset dp, const ui
   }
 }
 
-// ---- piece-list form (BK_LEGAL_WPB=41): only the (board, origin row, piece) triples that can ----
-// hold a legal placement. A row r can only be the origin row of a legal placement when rows
-// r..r+4 hold a free anchor cell (anchor & ~forbidden), and only the mover's unused pieces can be
-// placed; on mid-game 20x20 boards that leaves ~60% of the rows and ~half of the pieces, so the
-// row-parallel form above spends most of its lane-orientations on fields known to be empty.
-// Here a workgroup of 4 waves holds BPW boards (8 by default), builds per piece a list of the
-// (board, row) pairs that qualify, and each wave task evaluates ONE piece's orientations (a
-// compile-time switch: the same unrolled cell offsets) for 64 list entries — every lane its own
-// board and row — ORing non-empty fields into its board's LDS mask.
-constexpr int kPieceRows = kMaxN + 4;  // frar rows r..r+4 stay inside the board's slice
-struct PieceFirst {
-  int o[kNumPieces + 1];
-};
-constexpr PieceFirst make_piece_first() {
-  PieceFirst t{};
-  int o = 0;
-  for (int p = 0; p <= kNumPieces; ++p) {
-    while (o < kNumOrient && kOrient[o].piece < p) ++o;
-    t.o[p] = o;
-  }
-  return t;
-}
-constexpr PieceFirst kPieceFirst = make_piece_first();
-
-struct PieceLane {
-  uint32_t fr[5], ar[5];
-  uint32_t rowok[6];
-  int r, rN1;
-  uint32_t* mb;
-};
-template <int O>
-__device__ __forceinline__ void piece_orient(const DevPreset& dp, const PieceLane& c) {
-  constexpr OrientC oc = kOrient[O];
-  const int N = dp.N;
-  const int W = N - oc.w + 1;
-  uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
-  uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
-#pragma unroll
-  for (int k = 1; k < oc.n; ++k) {
-    bad |= c.fr[oc.dr[k]] << oc.dc[k];
-    good |= c.ar[oc.dr[k]] << oc.dc[k];
-  }
-  const uint32_t v = __brev(good & ~bad) & ((1u << W) - 1u) & c.rowok[oc.h];
-  if (v) {
-    const int bit = kOrientBase.cnt[O] * N * N + kOrientBase.b[O] * N + kOrientBase.c[O] + c.rN1 - c.r * oc.w;
-    const uint64_t x = (uint64_t)v << (bit & 31);
-    uint32_t* dst = c.mb + (bit >> 5);
-    atomicOr(dst, (uint32_t)x);
-    if ((uint32_t)(x >> 32)) atomicOr(dst + 1, (uint32_t)(x >> 32));
-  }
-}
-template <int P, size_t... Ks>
-__device__ __forceinline__ void piece_orients(const DevPreset& dp, const PieceLane& c, std::index_sequence<Ks...>) {
-  (piece_orient<kPieceFirst.o[P] + (int)Ks>(dp, c), ...);
-}
-template <size_t... Ps>
-__device__ __forceinline__ void piece_dispatch(const DevPreset& dp, const PieceLane& c, int p,
-                                               std::index_sequence<Ps...>) {
-  // p is wave-uniform: one compare-and-branch per piece, then that piece's orientations unrolled
-  ((p == (int)Ps ? piece_orients<(int)Ps>(dp, c, std::make_index_sequence<kPieceFirst.o[Ps + 1] - kPieceFirst.o[Ps]>{})
-                 : void()),
-   ...);
-}
-
-// Grid: ceil(B / BPW) blocks of 256 threads. Requires BPW * N <= 256.
-template <int BPW>
-__global__ __launch_bounds__(256) void k_legal_mask_pieces(DevPreset dp, const uint32_t* __restrict__ states,
-                                                           const int32_t* __restrict__ players, int B,
-                                                           uint64_t* __restrict__ masks,
-                                                           int32_t* __restrict__ counts) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t m32[];      // [BPW][W32pad]
-  __shared__ __attribute__((aligned(16))) uint32_t st_sh[BPW * kStateWords];
-  __shared__ uint2 frar[BPW * kPieceRows];                             // (fr, ar) per row, bit-reversed
-  __shared__ uint8_t items[kNumPieces][BPW * kMaxN];                  // (board, row) = b * N + r
-  __shared__ int cnt_sh[kNumPieces];
-  __shared__ int any_sh[BPW];
-  __shared__ int bcnt[BPW];
-  const int tid = threadIdx.x;
-  const int l = lane_id();
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int N = dp.N;
-  const int b0 = blockIdx.x * BPW;
-  const int nb = B - b0 < BPW ? B - b0 : BPW;
-  // (1) the boards' states, coalesced; masks and lists zeroed
-  for (int i = tid; i < nb * kStateWords / 4; i += 256)
-    reinterpret_cast<uint4*>(st_sh)[i] = reinterpret_cast<const uint4*>(states + (size_t)b0 * kStateWords)[i];
-  for (int i = tid; i < BPW * dp.W32pad / 4; i += 256) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
-  for (int i = tid; i < BPW * kPieceRows; i += 256) frar[i] = make_uint2(0u, 0u);
-  if (tid < kNumPieces) cnt_sh[tid] = 0;
-  if (tid < BPW) {
-    any_sh[tid] = 0;
-    bcnt[tid] = 0;
-  }
-  const int b = tid / N;  // one thread per (board, row)
-  const int r = tid - b * N;
-  const bool ok = b < nb;
-  int q = 0;
-  if (ok) {
-    q = players ? players[b0 + b] : -1;
-  }
-  __syncthreads();
-  const uint32_t* s = st_sh + (ok ? b : 0) * kStateWords;
-  if (ok && q < 0) q = (int)s[kWToMove];
-  const uint32_t own = ok ? s[q * kMaxN + r] : 0u;
-  if (own) any_sh[b] = 1;
-  __syncthreads();
-  // (2) forbidden / anchor rows of the mover
-  if (ok) {
-    const uint32_t occ = s[r] | s[kMaxN + r] | s[2 * kMaxN + r] | s[3 * kMaxN + r];
-    const uint32_t up = r > 0 ? s[q * kMaxN + r - 1] : 0u;
-    const uint32_t dn = r + 1 < N ? s[q * kMaxN + r + 1] : 0u;
-    const uint32_t forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
-    const uint32_t anch = any_sh[b] ? ((up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row)
-                                    : (r == dp.corner_r[q] ? (1u << dp.corner_c[q]) : 0u);
-    frar[b * kPieceRows + r] = make_uint2(__brev(forb), __brev(anch));
-  }
-  __syncthreads();
-  // (3) per piece, the (board, row) pairs with a free anchor in rows r..r+4 and the piece unused
-  bool act = false;
-  if (ok) {
-#pragma unroll
-    for (int d = 0; d < 5; ++d) {
-      const uint2 v = frar[b * kPieceRows + r + d];
-      act |= (v.y & ~v.x) != 0u;
-    }
-  }
-  const uint32_t want = act ? (s[kWPieces + q] & ((1u << dp.num_pieces) - 1u)) : 0u;
-  const uint64_t lt = (1ull << l) - 1ull;
-  if (__ballot(want != 0u)) {
-    for (int p = 0; p < dp.num_pieces; ++p) {
-      const bool w = (want >> p) & 1u;
-      const uint64_t m = __ballot(w);
-      if (!m) continue;
-      int base = 0;
-      if (l == 0) base = atomicAdd(&cnt_sh[p], __popcll(m));
-      base = __shfl(base, 0, kWave);
-      if (w) items[p][base + __popcll(m & lt)] = (uint8_t)tid;
-    }
-  }
-  __syncthreads();
-  // (4) wave tasks: (piece, 64 entries of its list), dealt round robin over the 4 waves
-  int task = 0;
-  for (int p = 0; p < dp.num_pieces; ++p) {
-    const int n = __builtin_amdgcn_readfirstlane(cnt_sh[p]);
-    for (int i0 = 0; i0 < n; i0 += kWave, ++task) {
-      if ((task & 3) != wave) continue;
-      const bool live = i0 + l < n;
-      const int it = live ? items[p][i0 + l] : 0;
-      const int bb = it / N;
-      const int rr = it - bb * N;
-      PieceLane e;
-#pragma unroll
-      for (int d = 0; d < 5; ++d) {
-        const uint2 v = frar[bb * kPieceRows + rr + d];
-        e.fr[d] = v.x;
-        e.ar[d] = v.y;
-      }
-#pragma unroll
-      for (int h = 0; h < 6; ++h) e.rowok[h] = (live && rr + h <= N) ? ~0u : 0u;
-      e.r = rr;
-      e.rN1 = rr * (N + 1);
-      e.mb = m32 + bb * dp.W32pad;
-      piece_dispatch(dp, e, p, std::make_index_sequence<kNumPieces>{});
-    }
-  }
-  __syncthreads();
-  // (5) stream the masks out (16-B rows when W64 is even), popcounts per board
-  for (int jj = 0; jj < nb; ++jj) {
-    int cnt = 0;
-    if ((dp.W64 & 1) == 0) {
-      const uint4* src = reinterpret_cast<const uint4*>(m32 + jj * dp.W32pad);
-      uint4* dst = reinterpret_cast<uint4*>(masks + (size_t)(b0 + jj) * dp.W64);
-      for (int i = tid; i < dp.W64 / 2; i += 256) {
-        const uint4 v = src[i];
-        dst[i] = v;
-        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-      }
-    } else {
-      for (int i = tid; i < dp.W64; i += 256) {
-        const uint32_t* src = m32 + jj * dp.W32pad + 2 * i;
-        const uint64_t v = (uint64_t)src[0] | ((uint64_t)src[1] << 32);
-        masks[(size_t)(b0 + jj) * dp.W64 + i] = v;
-        cnt += __popcll(v);
-      }
-    }
-    cnt = wave_sum(cnt);
-    if (l == 0 && cnt) atomicAdd(&bcnt[jj], cnt);
-  }
-  __syncthreads();
-  if (counts && tid < nb) counts[b0 + tid] = bcnt[tid];
-}
-
 }  // namespace bk

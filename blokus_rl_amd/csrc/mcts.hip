@@ -279,163 +279,6 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
 #undef BK_OV_STAMP
 }
 
-// k_leaf_step_ov with the leaf logits shared out across workgroups (BK_STEP_STEAL=1; mcts_dev.h
-// lg_*): the logit waves claim chunks of their own tree's ids, then of other trees' still
-// unclaimed ids, so a tree with many legal ids no longer sets the launch alone. The wave that
-// finds its own tree's logits all done (lg_done[t] == K) copies them into LDS and writes the new
-// node's children (expand_children_lds, the same arithmetic); the rest is k_leaf_step_ov's.
-__global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ws(DevPreset dp, DevMcts m, const float* __restrict__ feat,
-                                                                    int64_t ldf, int F, const float* __restrict__ W,
-                                                                    const float* __restrict__ bias,
-                                                                    const float* __restrict__ values, int do_select,
-                                                                    const uint32_t* __restrict__ roots,
-                                                                    const int32_t* __restrict__ active, double cpuct,
-                                                                    int32_t* __restrict__ status_out,
-                                                                    float* __restrict__ obs,
-                                                                    uint64_t* __restrict__ mask_out, int sel_off) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ int status_sh, status0_sh;
-  __shared__ StepExpand sx;
-  const int t = blockIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (threadIdx.x == 0) {
-    sx.ready = 0;
-    sx.pready = 0;
-    sx.done = 0;
-    sx.leaf_ready = 0;
-    sx.slice = 0;
-    sx.loaded = 0;
-    sx.counted = 0;
-    sx.written = 0;
-    sx.kready = 0;
-    sx.hready = 0;
-    sx.expanding = 0;
-    status_sh = 0;
-    status0_sh = m.leaf_status[t];
-  }
-  __syncthreads();
-  const int status0 = status0_sh;
-  int K = -1;
-  if (wave > 0) {
-    K = leaf_logits_prologue_w<kStepWaves - 1, true>(dp, m, t, feat, ldf, F, lds, wave, &sx, status0);
-    if (wave == 1 && K >= 0) {
-      wait_flag_acquire(&sx.hready);
-      StepHead h;
-      h.status = sx.hd_status;
-      h.node = sx.hd_node;
-      h.used = sx.hd_used;
-      h.key = sx.hd_key;
-      expand_head(m, t, h, K, &sx);
-    }
-  }
-  const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
-  const float* fl = reinterpret_cast<const float*>(lds + dp.W32pad + kLeafCap);
-  float* lg = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap + F);
-  uint32_t* lsel = lds + sel_off;
-  uint32_t* m32 = lsel + kStateWords + 2 * kMaxN;
-  if (wave == 0) {
-    const StepHead h = backup_first(m, t, dp.P, values, status0);
-    if (h.status == 1) {
-      if (lane_id() == 0) {
-        sx.hd_status = h.status;
-        sx.hd_node = h.node;
-        sx.hd_used = h.used;
-        sx.hd_key = h.key;
-        __hip_atomic_store(&sx.hready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    } else if (lane_id() == 0) {
-      sx.err = -1;
-      __hip_atomic_store(&sx.ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (do_select) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      asm volatile("buffer_inv sc0" ::: "memory");
-      int* pend[3];
-      pend[0] = &sx.ready;
-      pend[1] = &sx.pready;
-      pend[2] = &sx.err;
-      const int st = select_descend(dp, m, t, roots, active, cpuct, status_out, lsel, h.key,
-                                    h.status == 1 ? pend : nullptr);
-      if (st == 1)
-        for (int i = lane_id(); i < dp.W32pad / 4; i += kWave) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
-      if (lane_id() == 0) {
-        status_sh = st;
-        __hip_atomic_store(&sx.leaf_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-  }
-  if (wave > 0) {
-    const bool own = K >= 0 && K <= kLeafCap;  // this tree has logits to compute (wave-uniform)
-    // the new node's children, once: every logit of the tree is stored (by any workgroup) and
-    // expand_head has published the node (ready); the claimant copies the logits into LDS and runs
-    // expand_children_lds. Returns true when this wave finished the expansion (or it is done).
-    auto try_expand = [&](bool wait) {
-      if (!own) return;
-      if (readlane_i(__hip_atomic_load(&sx.expanding, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0)) return;
-      for (;;) {
-        const uint32_t dn = (uint32_t)readlane_i(
-            (int)__hip_atomic_load(m.lg_done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0);
-        if (dn >= (uint32_t)K) break;
-        if (!wait) return;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      int won = 0;
-      if (lane_id() == 0) {
-        int z = 0;
-        won = __hip_atomic_compare_exchange_strong(&sx.expanding, &z, 1, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (!readlane_i(won, 0)) return;
-      while (__hip_atomic_load(&sx.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-        __builtin_amdgcn_s_sleep(1);
-      const int err = readlane_i(sx.err, 0);
-      if (err == 0) {
-        const float* gl = m.leaf_logit + (size_t)t * kLeafCap;
-        for (int i = lane_id(); i < K; i += kWave) lg[i] = ld_sc1_f32(gl + i);
-        wave_lds_sync();
-        expand_children_lds(m, (int64_t)sx.off, K, ids, lg);
-      }
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the children stored before the flag
-      if (lane_id() == 0) {
-        __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // the tree's work word back to "none" for the next step (every chunk is done)
-        __hip_atomic_store(m.lg_work + t, (unsigned long long)kLgNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(m.lg_done + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    };
-    if (own) {
-      while (__hip_atomic_load(&sx.kready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-        __builtin_amdgcn_s_sleep(1);
-      int lo, hi;
-      while (lg_claim(m, t, lo, hi)) {
-        lg_chunk<true>(m, t, lo, hi, W, bias, F, ids, fl);
-        lg_finish(m, t, hi - lo);
-      }
-      try_expand(false);
-    }
-    // then other trees' unclaimed chunks, the own expansion checked between them
-    for (;;) {
-      const int tt = lg_find(m, (t + 1 + 37 * wave) % m.T);
-      if (tt < 0) break;
-      int lo, hi;
-      if (lg_claim(m, tt, lo, hi)) {
-        lg_chunk<false>(m, tt, lo, hi, W, bias, F, nullptr, feat + (size_t)tt * ldf);
-        lg_finish(m, tt, hi - lo);
-      }
-      try_expand(false);
-    }
-    try_expand(true);  // the last chunks may still be with other workgroups
-  }
-  if (do_select) {
-    while (__hip_atomic_load(&sx.leaf_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-      __builtin_amdgcn_s_sleep(1);
-    if (readlane_i(status_sh, 0) == 1) mask_slices_claim(dp, lsel, m32, &sx.slice);
-  }
-  __syncthreads();
-  if (!do_select) return;
-  select_leaf<kStepWaves, true>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
-}
-
 __device__ __forceinline__ double raise_visits(uint32_t n, double e) {
   if (e == 1.0 || n <= 1u) return (double)n;
   return pow((double)n, e);
@@ -589,13 +432,6 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
   if (!rc) rc = mcts_alloc(m, &d.leaf_ids, T * kLeafCap);
   if (!rc) rc = mcts_alloc(m, &d.leaf_logit, T * kLeafCap);
   if (!rc) rc = mcts_alloc(m, &d.leaf_K, T);
-  if (!rc) rc = mcts_alloc(m, &d.lg_work, T);
-  if (!rc) rc = mcts_alloc(m, &d.lg_done, T);
-  if (!rc) {  // work words "none" (K = 0xFFFFFFFF, next 0), counts 0
-    std::vector<unsigned long long> none(T, (unsigned long long)kLgNone);
-    rc = hip_check(hipMemcpy(d.lg_work, none.data(), T * sizeof(unsigned long long), hipMemcpyHostToDevice), "init lg_work");
-  }
-  if (!rc) rc = hip_check(hipMemset(d.lg_done, 0, T * sizeof(uint32_t)), "memset lg_done");
   if (!rc) rc = mcts_alloc(m, &d.counters, 8);
   if (!rc) rc = hip_check(hipMemset(d.counters, 0, 8 * sizeof(unsigned long long)), "memset counters");
   if (!rc) rc = mcts_alloc(m, &d.tree_ctr, T * 8);
@@ -660,15 +496,6 @@ int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const f
   const DevPreset& dp = m->ctx->dp;
   const char* ov = getenv("BK_STEP_OVERLAP");  // read per call (graph capture reads it once)
   const int overlap = ov ? atoi(ov) : 1;
-  const char* stl = getenv("BK_STEP_STEAL");   // A/B: logits shared out across workgroups
-  if (overlap && stl && atoi(stl)) {
-    const int sel_off = (int)(((size_t)dp.W32pad + 2 * kLeafCap + F + 3) & ~(size_t)3);
-    const size_t words = (size_t)sel_off + kStateWords + 2 * kMaxN + dp.W32pad;
-    hipLaunchKernelGGL(k_leaf_step_ws, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
-                       (hipStream_t)stream, dp, m->d, feat, ldf, F, W, bias, values, do_select,
-                       (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, sel_off);
-    return launch_check("k_leaf_step_ws");
-  }
   if (overlap) {
     const int sel_off = (int)(((size_t)dp.W32pad + 2 * kLeafCap + F + 3) & ~(size_t)3);
     const size_t words = (size_t)sel_off + kStateWords + 2 * kMaxN + dp.W32pad;

@@ -63,8 +63,6 @@ struct DevMcts {
   int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
   float* leaf_logit;    // [T*kLeafCap] their logits
   int32_t* leaf_K;      // [T]
-  unsigned long long* lg_work;  // [T] k_leaf_step_ws: next id to claim << 32 | published K (0xFFFFFFFF: none)
-  uint32_t* lg_done;            // [T] k_leaf_step_ws: logits computed
   unsigned long long* counters;  // [8] (errors; the totals when BK_TREE_CTR is 0)
   unsigned long long* tree_ctr;  // [T*8] per-tree counters: uncontended atomics, summed on read
 };
@@ -723,7 +721,6 @@ struct StepExpand {
   int kready;     // the leaf's legal ids are compacted: K + 1 (1 + -1 = 0 is never published)
   int hready;     // wave 0 published hd (its backup is done)
   int wcnt[16];   // legal ids per logit wave's 64-word segment of the leaf bitmask
-  int expanding;  // k_leaf_step_ws: the wave that writes the new node's children claimed the role
   int hd_status, hd_node;
   long long hd_used;
   unsigned long long hd_key;
@@ -825,9 +822,7 @@ __device__ __forceinline__ void expand_head(const DevMcts& m, int t, const StepH
 // bitmask, offsets from the segment counts: the ids in ascending order, as compact_ids writes
 // them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32. status: the leaf status
 // the step started from (not m.leaf_status, which wave 0's next descent rewrites meanwhile).
-// SHARE (k_leaf_step_ws): the ids also go to leaf_ids (write-through) and wave 1 publishes the
-// tree's logit work word (K) before kready.
-template <int NW, bool SHARE = false>
+template <int NW>
 __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const DevMcts& m, int t,
                                                       const float* __restrict__ feat, int64_t ldf, int F,
                                                       uint32_t* lds, int wave, StepExpand* sx, int status) {
@@ -863,24 +858,16 @@ __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const
     K += c;
   }
   int pos = before + incl - cnt;
-  int32_t* gids = m.leaf_ids + (size_t)t * kLeafCap;
   while (bits) {
     const int b = __ffs(bits) - 1;
     bits &= bits - 1u;
-    if (pos < kLeafCap) {
-      ids[pos] = w * 32 + b;
-      if (SHARE) __hip_atomic_store(gids + pos, w * 32 + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (pos < kLeafCap) ids[pos] = w * 32 + b;
     ++pos;
   }
-  if (SHARE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's id stores are done
   arrive_wait(&sx->written);
   if (wave == 1 && l == 0) {
     m.leaf_K[t] = K;
     if (K > kLeafCap) atomicOr(&m.counters[kCtrErr], (unsigned long long)kErrLeafCap);
-    // every logit wave's id stores completed before it arrived: publish the work (next 0, K)
-    if (SHARE && K <= kLeafCap)
-      __hip_atomic_store(m.lg_work + t, (unsigned long long)(unsigned)K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&sx->kready, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   return K;
@@ -953,106 +940,6 @@ __device__ __forceinline__ void expand_children_lds(const DevMcts& m, int64_t of
     m.ch_Q[off + i] = 0.0;
     m.ch_P[off + i] = expf((lg[i] - mx) - lse);
   }
-}
-
-// ---- k_leaf_step_ws: k_leaf_step_ov with the leaf logits shared out across workgroups. A tree's
-// logit work (K rows of the policy Linear, 3.2 KB each at 20x20: the step's longest phase, set by
-// the tree with the most legal ids) is claimed in chunks of kLgChunk ids from a per-tree work word
-// (next << 32 | K, one agent-scope atomic add per claim); a workgroup whose own tree is done claims
-// chunks of other trees. The ids travel to global memory (leaf_ids) before K is published, the
-// logits go to leaf_logit, and the owner expands its node once lg_done[t] reaches K. Hand-offs
-// between workgroups use write-through (sc1) stores, a vmcnt(0) wait, then the agent-scope atomic
-// that publishes, and sc1 loads on the reading side (MI355X_MICROARCH.md, inter-workgroup
-// visibility). The logits are summed exactly as leaf_logits_dots does: the trees are bitwise those
-// of k_leaf_step_ov.
-constexpr int kLgChunk = 32;
-constexpr unsigned kLgNone = 0xFFFFFFFFu;
-
-__device__ __forceinline__ void st_sc1_f32(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1_i32(int32_t* p, int32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int32_t ld_sc1_i32(const int32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1_f32(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The logits of ids [lo, hi) of tree tt by one wave: 4 ids at a time, 16 lanes each, the streaming
-// sums of leaf_logits_dots (same order, bitwise); ids from LDS (own tree) or global (sc1), the
-// features from LDS (own) or global; each logit stored write-through to leaf_logit.
-template <bool OWN>
-__device__ __forceinline__ void lg_chunk(const DevMcts& m, int tt, int lo, int hi, const float* __restrict__ W,
-                                         const float* __restrict__ bias, int F, const int32_t* ids_lds,
-                                         const float* feat_src) {
-  const int l = lane_id(), sub = l & 15, quad = l >> 4;
-  const int F4 = F >> 2;
-  const float4* f4 = reinterpret_cast<const float4*>(feat_src);
-  const int32_t* gids = m.leaf_ids + (size_t)tt * kLeafCap;
-  float* out = m.leaf_logit + (size_t)tt * kLeafCap;
-  for (int j0 = lo; j0 < hi; j0 += 4) {
-    const int j = j0 + quad;
-    const bool ok = j < hi;
-    const int jj = ok ? j : lo;
-    const int id = OWN ? ids_lds[jj] : ld_sc1_i32(gids + jj);
-    const float4* r = reinterpret_cast<const float4*>(W + (size_t)id * F);
-    float a0 = 0.f, a1 = 0.f;
-    int q = sub;
-    for (; q + 48 < F4; q += 64) {
-      const float4 w0 = r[q], w1 = r[q + 16], w2 = r[q + 32], w3 = r[q + 48];
-      const float4 x0 = f4[q], x1 = f4[q + 16], x2 = f4[q + 32], x3 = f4[q + 48];
-      a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
-      a1 += w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
-      a0 += w2.x * x2.x + w2.y * x2.y + w2.z * x2.z + w2.w * x2.w;
-      a1 += w3.x * x3.x + w3.y * x3.y + w3.z * x3.z + w3.w * x3.w;
-    }
-    for (; q < F4; q += 16) {
-      const float4 w0 = r[q], x0 = f4[q];
-      a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
-    }
-    float a = a0 + a1;
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
-    if (sub == 0 && ok) st_sc1_f32(out + j, a + bias[id]);
-  }
-}
-
-// Claim the next chunk of tree tt: [lo, hi) or false (nothing left / not published)
-__device__ __forceinline__ bool lg_claim(const DevMcts& m, int tt, int& lo, int& hi) {
-  unsigned long long old = 0;
-  if (lane_id() == 0)
-    old = __hip_atomic_fetch_add(m.lg_work + tt, (unsigned long long)kLgChunk << 32, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-  old = readlane_u64(old, 0);
-  const unsigned K = (unsigned)old, next = (unsigned)(old >> 32);
-  if (K == kLgNone || next >= K) return false;
-  lo = (int)next;
-  hi = (int)(next + kLgChunk < K ? next + kLgChunk : K);
-  return true;
-}
-// logits [lo, hi) of tree tt are stored: count them (after this wave's stores are complete)
-__device__ __forceinline__ void lg_finish(const DevMcts& m, int tt, int n) {
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the write-through logit stores are done
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane_id() == 0) __hip_atomic_fetch_add(m.lg_done + tt, (uint32_t)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// A tree with unclaimed published work, scanning from `start` (64 work words per load); -1: none
-__device__ __forceinline__ int lg_find(const DevMcts& m, int start) {
-  const int l = lane_id();
-  for (int b = 0; b < m.T; b += kWave) {
-    const int tt = (start + b + l) % m.T;
-    bool has = false;
-    if (b + l < m.T) {
-      const unsigned long long w = __hip_atomic_load(m.lg_work + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      has = (unsigned)w != kLgNone && (unsigned)(w >> 32) < (unsigned)w;
-    }
-    const uint64_t bal = __ballot(has);
-    if (bal) return readlane_i(tt, __ffsll((unsigned long long)bal) - 1);
-  }
-  return -1;
 }
 
 }  // namespace bk

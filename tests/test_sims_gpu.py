@@ -16,16 +16,13 @@ def _leaf_model(eng, blocks=2, seed=0):
     return LeafResNet(net, normalize=False, features=True).eval()
 
 
-@pytest.mark.parametrize("N,T,sims,overlap", [(20, 12, 9, "1"), (20, 12, 9, "0"), (14, 7, 6, "1"), (20, 64, 40, "1"),
-                                            (20, 12, 9, "ws"), (14, 7, 6, "ws"), (20, 64, 40, "ws")])
+@pytest.mark.parametrize("N,T,sims,overlap", [(20, 12, 9, "1"), (20, 12, 9, "0"), (14, 7, 6, "1"), (20, 64, 40, "1")])
 def test_leaf_step_matches_stagewise(N, T, sims, overlap, monkeypatch):
     """bk_mcts_leaf_step (policy head + expand/backup + the next descent in one launch; overlap 1
     = k_leaf_step_ov, the default, whose wave 0 backs up and descends while the other waves
-    compute the logits; ws = k_leaf_step_ws, the logits shared out across workgroups) against
-    k_leaf_logits -> k_expand_backup -> k_select: the same trees, counters, leaf states and
-    observations, bitwise."""
-    monkeypatch.setenv("BK_STEP_OVERLAP", "0" if overlap == "0" else "1")
-    monkeypatch.setenv("BK_STEP_STEAL", "1" if overlap == "ws" else "0")
+    compute the logits) against k_leaf_logits -> k_expand_backup -> k_select: the same trees,
+    counters, leaf states and observations, bitwise."""
+    monkeypatch.setenv("BK_STEP_OVERLAP", overlap)
     from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
     from blokus_rl_amd.boards import random_boards
     from blokus_rl_amd.engine import Engine
