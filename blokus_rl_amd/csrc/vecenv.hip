@@ -178,7 +178,8 @@ struct Vec7 {
   static constexpr int W64 = (A + 63) / 64, W32 = (A + 31) / 32;
 };
 // per orientation: cells at stride 8 packed 6 bits each (unused cells repeat cell 0), valid
-// origins, first id | piece << 12 | origin columns W << 17 | height h << 20
+// origins, first id | piece << 12 | origin columns W << 17 | height h << 20 | ceil(256 / W) << 23
+// (rel / W = (rel * ceil(256 / W)) >> 8 for every rel < 64, W <= 7)
 struct Or7 {
   uint32_t offs, meta;
   uint64_t valid;
@@ -196,7 +197,10 @@ struct Or7Table {
       uint64_t valid = 0;
       for (int r = 0; r < R; ++r)
         for (int c = 0; c < W; ++c) valid |= 1ull << (r * 8 + c);
-      o[k] = Or7{offs, (uint32_t)id | ((uint32_t)q.piece << 12) | ((uint32_t)W << 17) | ((uint32_t)q.h << 20), valid};
+      o[k] = Or7{offs,
+                 (uint32_t)id | ((uint32_t)q.piece << 12) | ((uint32_t)W << 17) | ((uint32_t)q.h << 20) |
+                     ((uint32_t)((256 + W - 1) / W) << 23),
+                 valid};
       id += R * W;
     }
   }
@@ -257,19 +261,20 @@ __device__ __forceinline__ int grp_incl(int x, int j) {
   return x;
 }
 // bit index of the k-th (0-based) set bit of x (k < popcount(x)): binary search on popcounts
-__device__ __forceinline__ int kth_bit64(uint64_t x, int k) {
-  int pos = 0;
+__device__ __forceinline__ int kth_bit64(uint64_t x64, int k) {
+  const int c0 = __popc((uint32_t)x64);
+  const bool up = k >= c0;
+  uint32_t x = up ? (uint32_t)(x64 >> 32) : (uint32_t)x64;  // 32-bit ops from here
+  int pos = up ? 32 : 0;
+  k = up ? k - c0 : k;
 #pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const uint64_t lo = x & ((1ull << w) - 1ull);
-    const int c = __popcll(lo);
-    if (k >= c) {
-      k -= c;
-      x >>= w;
-      pos += w;
-    } else {
-      x = lo;
-    }
+  for (int w = 16; w >= 1; w >>= 1) {
+    const uint32_t lo = x & ((1u << w) - 1u);
+    const int c = __popc(lo);
+    const bool u = k >= c;
+    k = u ? k - c : k;
+    x = u ? x >> w : lo;
+    pos += u ? w : 0;
   }
   return pos;
 }
@@ -305,9 +310,10 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   const int e = e0 + le;
   const bool live = e < E;
   const int es = live ? e : E - 1;  // a spare lane group mirrors the last env and stores nothing
+  for (int w = j; w < V::W32 + 1; w += G) m32[le][w] = 0u;  // the env's mask words (its own lanes)
 
   // this lane's orientations (8 i + j): cells, valid origins, meta
-  uint32_t offs[NL], meta[NL];
+  uint32_t offs[NL], meta[NL], off[NL][MC];
   uint64_t valid[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
@@ -316,6 +322,8 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     offs[i] = q.offs;
     meta[i] = q.meta;
     valid[i] = k < V::NO ? q.valid : 0ull;
+#pragma unroll
+    for (int c = 0; c < MC; ++c) off[i][c] = (q.offs >> (6 * c)) & 63u;  // cells past the piece repeat cell 0
   }
   // the state words of a 7x7 / 2-colour game
   const uint32_t* g = states + (size_t)es * kStateWords;
@@ -349,10 +357,9 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     for (int i = 0; i < NL; ++i) {
       uint64_t fo = 0, ao = 0;
 #pragma unroll
-      for (int k = 0; k < MC; ++k) {  // cells past the piece's size repeat cell 0
-        const int off = (int)((offs[i] >> (6 * k)) & 63u);
-        fo |= F >> off;
-        ao |= A >> off;
+      for (int k = 0; k < MC; ++k) {
+        fo |= F >> off[i][k];
+        ao |= A >> off[i][k];
       }
       const bool have = (pieces[q] >> ((meta[i] >> 12) & 31u)) & 1u;
       L[i] = have ? (valid[i] & ~fo & ao) : 0ull;
@@ -372,10 +379,19 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     int before = 0;
     uint64_t sel = 0;  // id | org << 16 from the owning lane
     uint32_t so = 0, sm = 0;
+    // orientations i, i + 1 scanned together: counts (<= 49 each, <= 784 per group) in 16-bit halves
+    int inclp[(NL + 1) / 2], totp[(NL + 1) / 2];
+#pragma unroll
+    for (int h = 0; h < (NL + 1) / 2; ++h) {
+      const int x = __popcll(L[2 * h]) | (2 * h + 1 < NL ? __popcll(L[2 * h + 1]) << 16 : 0);
+      inclp[h] = grp_incl<G>(x, j);
+      totp[h] = grp_sum<G>(x);
+    }
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = __popcll(L[i]);
-      const int incl = grp_incl<G>(c, j), tot = grp_sum<G>(c);
+      const int sh = 16 * (i & 1);
+      const int incl = (inclp[i / 2] >> sh) & 0xFFFF, tot = (totp[i / 2] >> sh) & 0xFFFF;
       const int kk = k - before - (incl - c);
       if (kk >= 0 && kk < c) {
         const int pos = kth_bit64(L[i], kk);
@@ -401,7 +417,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
       const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u), h = (int)((meta[i] >> 20) & 7u);
       const int rel = a - base;
       if (valid[i] && rel >= 0 && rel < (8 - h) * W) {
-        const int r = rel / W, c = rel - r * W;
+        const int r = (rel * (int)(meta[i] >> 23)) >> 8, c = rel - r * W;
         if ((L[i] >> (r * 8 + c)) & 1ull) {
           sel = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)(r * 8 + c) << 16) | (1ull << 63);
           so = offs[i];
@@ -495,8 +511,6 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   VSTAMP(4);
 
   // ---- outputs: the state words, rng, reward, done (lanes 0..3 of the env's group); obs and mask via LDS
-  for (int w = tid; w < kVecEnvsPerBlock * (V::W32 + 1); w += kVecThreads) (&m32[0][0])[w] = 0u;
-  __syncthreads();
   if (live) {
     uint32_t* gs = states + (size_t)e * kStateWords;
     if (j == 0) {
@@ -526,18 +540,22 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
 #pragma unroll
       for (int c = 0; c < 7; ++c) ob[le * 49 + j * 7 + c] = ((r0 >> c) & 1u) ? 1 : (((r1 >> c) & 1u) ? 2 : 0);
     }
-    // mask: each legal origin row of the lane's orientations ORed into the env's LDS words
+    // mask: each orientation's legal origins compacted from stride-8 rows to its (R x W)-bit field
+    // (<= 49 bits), ORed into the env's LDS words at the orientation's first id (<= 3 words)
+    wave_lds_sync();  // the group's zeroing of its words (kernel start) is done
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u);
+      uint64_t f = 0;
 #pragma unroll
-      for (int r = 0; r < 7; ++r) {
-        const uint32_t bits = (uint32_t)(L[i] >> (8 * r)) & 0x7Fu;
-        if (bits) {
-          const int pos = base + r * W, w = pos >> 5, sh = pos & 31;
-          atomicOr(&m32[le][w], bits << sh);
-          if (sh + W > 32) atomicOr(&m32[le][w + 1], bits >> (32 - sh));
-        }
+      for (int r = 0; r < 7; ++r) f |= (uint64_t)((uint32_t)(L[i] >> (8 * r)) & 0x7Fu) << (r * W);
+      if (f) {
+        const int w = base >> 5, sh = base & 31;
+        const uint64_t x = f << sh;
+        const uint32_t x2 = sh ? (uint32_t)(f >> (64 - sh)) : 0u;
+        if ((uint32_t)x) atomicOr(&m32[le][w], (uint32_t)x);
+        if ((uint32_t)(x >> 32)) atomicOr(&m32[le][w + 1], (uint32_t)(x >> 32));
+        if (x2) atomicOr(&m32[le][w + 2], x2);
       }
     }
   }

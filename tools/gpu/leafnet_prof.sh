@@ -16,4 +16,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE S
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-trace -d $out/p$i -o c --output-format csv -- python tools/leafnet_bench.py 5 256 > $out/p$i.log 2>&1 || exit 1
 done
-python tools/pmc_to_json.py gpurun_out/r02_pmc_leafnet.json k_leafnet_x3 k_leafnet_x3 256 0 "rocprofv3 --pmc passes of tools/leafnet_bench.py" $out/p*
+python tools/pmc_to_json.py gpurun_out/r04_pmc_leafnet.json k_leafnet_x3 k_leafnet_x3 256 0 "rocprofv3 --pmc passes of tools/leafnet_bench.py" $out/p*
