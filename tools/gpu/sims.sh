@@ -1,5 +1,5 @@
 #!/bin/bash
-# Fused simulations: k_sims parity + search/self-play/conv GPU tests, the self-play bench line, and
+# Search, self-play and conv GPU tests (the fused leaf step and graph replay), the self-play bench line, and
 # its kernel-trace summary.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
