@@ -62,6 +62,7 @@ struct DevMcts {
   uint64_t* leaf_mask;  // [T*W64] internal copy of the leaf bitmask
   int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
   float* leaf_logit;    // [T*kLeafCap] their logits
+  float* lg_dense;      // [T*A] the leaf logits by id (k_leaf_logits_ids; only the leaf's legal ids are written)
   int32_t* leaf_K;      // [T]
   unsigned long long* counters;  // [8] (errors; the totals when BK_TREE_CTR is 0)
   unsigned long long* tree_ctr;  // [T*8] per-tree counters: uncontended atomics, summed on read
@@ -429,6 +430,33 @@ __device__ __forceinline__ int leaf_logits_prologue(const DevPreset& dp, const D
 // The logits of ids [lo, hi) of the prologue's LDS id list by wave `wave` of nw: logit j to
 // out_lg[j] (global or LDS), its id to out_ids[j] when out_ids is given. Every logit is summed in
 // the same order whichever wave takes it, so any wave split gives the same values, bitwise.
+
+// One logit's dot product W[id] . f by the 16 lanes of a quarter wave (sub = lane & 15): a lane
+// sums every 16th float4 — whole trips of four alternate two partial sums, the rest go to the
+// first — and the 16 partial sums meet in 4 xor-shuffles. The single definition of the leaf
+// logits' arithmetic: k_leaf_logits, the fused leaf steps and k_leaf_logits_ids all sum through it,
+// so their logits agree bitwise whether f is in LDS or in global memory.
+__device__ __forceinline__ float row_dot16(const float4* __restrict__ r, const float4* f4, int F4, int sub) {
+  float a0 = 0.f, a1 = 0.f;
+  int q = sub;
+  for (; q + 48 < F4; q += 64) {
+    const float4 w0 = r[q], w1 = r[q + 16], w2 = r[q + 32], w3 = r[q + 48];
+    const float4 x0 = f4[q], x1 = f4[q + 16], x2 = f4[q + 32], x3 = f4[q + 48];
+    a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
+    a1 += w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
+    a0 += w2.x * x2.x + w2.y * x2.y + w2.z * x2.z + w2.w * x2.w;
+    a1 += w3.x * x3.x + w3.y * x3.y + w3.z * x3.z + w3.w * x3.w;
+  }
+  for (; q < F4; q += 16) {
+    const float4 w0 = r[q], x0 = f4[q];
+    a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
+  }
+  float a = a0 + a1;
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
+  return a;
+}
+
 template <int R = 1>
 __device__ __forceinline__ void leaf_logits_dots(const DevPreset& dp, int lo, int hi, int wave, int nw,
                                                  const float* __restrict__ W, const float* __restrict__ bias, int F,
@@ -490,24 +518,7 @@ __device__ __forceinline__ void leaf_logits_dots(const DevPreset& dp, int lo, in
       const int j = j0 + quad;
       const bool ok = j < hi;
       const int id = ids[ok ? j : lo];
-      const float4* r = reinterpret_cast<const float4*>(W + (size_t)id * F);
-      float a0 = 0.f, a1 = 0.f;
-      int q = sub;
-      for (; q + 48 < F4; q += 64) {
-        const float4 w0 = r[q], w1 = r[q + 16], w2 = r[q + 32], w3 = r[q + 48];
-        const float4 x0 = f4[q], x1 = f4[q + 16], x2 = f4[q + 32], x3 = f4[q + 48];
-        a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
-        a1 += w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
-        a0 += w2.x * x2.x + w2.y * x2.y + w2.z * x2.z + w2.w * x2.w;
-        a1 += w3.x * x3.x + w3.y * x3.y + w3.z * x3.z + w3.w * x3.w;
-      }
-      for (; q < F4; q += 16) {
-        const float4 w0 = r[q], x0 = f4[q];
-        a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
-      }
-      float a = a0 + a1;
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) a += __shfl_xor(a, o, 16);
+      const float a = row_dot16(reinterpret_cast<const float4*>(W + (size_t)id * F), f4, F4, sub);
       if (sub == 0 && ok) {
         if (out_ids) out_ids[j] = id;
         out_lg[j] = a + bias[id];
@@ -822,7 +833,7 @@ __device__ __forceinline__ void expand_head(const DevMcts& m, int t, const StepH
 // bitmask, offsets from the segment counts: the ids in ascending order, as compact_ids writes
 // them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32. status: the leaf status
 // the step started from (not m.leaf_status, which wave 0's next descent rewrites meanwhile).
-template <int NW>
+template <int NW, bool FEAT = true>
 __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const DevMcts& m, int t,
                                                       const float* __restrict__ feat, int64_t ldf, int F,
                                                       uint32_t* lds, int wave, StepExpand* sx, int status) {
@@ -837,8 +848,10 @@ __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const
     m32[2 * j] = (uint32_t)w;
     m32[2 * j + 1] = (uint32_t)(w >> 32);
   }
-  const float* ft = feat + (size_t)t * ldf;
-  for (int i = tid; i < F; i += nth) f[i] = ft[i];
+  if (FEAT) {  // the features for the logit dots (not when the logits come precomputed)
+    const float* ft = feat + (size_t)t * ldf;
+    for (int i = tid; i < F; i += nth) f[i] = ft[i];
+  }
   auto arrive_wait = [&](int* ctr) {  // a barrier of the NW logit waves (LDS counter)
     if (l == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NW) __builtin_amdgcn_s_sleep(1);

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(64) void k_vec_step(DevPreset dp, uint32_t* states,
 // to the G lanes of an env (orientation G i + j to lane j: 2 per lane for the 919-id preset, 6
 // for the 2522-id one at G = 16), each lane holding its orientations' cells / valid origins / id base in
 // registers. Counting, the k-th legal id (ascending id = ascending orientation, then origin bit
-// r*8 + c, as the bitmask order), hash updates and the legal-move mask are per-lane work met by
+// r*8 + c, as the bitmask order), the board hash (recomputed from the final board, one row key per lane) and the legal-move mask are per-lane work met by
 // 3- or 4-step DPP butterflies inside the env's lanes; obs and mask are staged in LDS and leave as coalesced
 // rows. Only the state words a 2-colour 7x7 game uses are read and written (occupancy rows 0..6
 // of colours 0 and 1, pieces, hash, to-move, ply, flags); the rest of the 384-B state stays as
@@ -236,6 +236,14 @@ __device__ __forceinline__ uint64_t grp_red64(uint64_t x, OP op) {
     hi = op(hi, dppu<0x140>(hi));
   }
   return ((uint64_t)hi << 32) | lo;
+}
+template <int G>
+__device__ __forceinline__ uint32_t grp_or32(uint32_t x) {
+  x |= dppu<0xB1>(x);
+  x |= dppu<0x4E>(x);
+  x |= dppu<0x141>(x);
+  if (G == 16) x |= dppu<0x140>(x);
+  return x;
 }
 template <int G>
 __device__ __forceinline__ uint64_t grp_or64(uint64_t x) {
@@ -339,7 +347,6 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   const uint4 w80 = *reinterpret_cast<const uint4*>(g + kWPieces);  // pieces of colours 0..3
   const uint4 w84 = *reinterpret_cast<const uint4*>(g + kWHash);    // hash lo, hi, to-move, ply
   uint32_t pieces[2] = {w80.x, w80.y};
-  uint64_t hash = (uint64_t)w84.x | ((uint64_t)w84.y << 32);
   int to_move = (int)w84.z;
   uint32_t ply = w84.w, flags = g[kWFlags];
   uint64_t st = rng[es];
@@ -377,7 +384,7 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   };
   auto kth = [&](int k) {
     int before = 0;
-    uint64_t sel = 0;  // id | org << 16 from the owning lane
+    uint32_t sel = 0;  // id | org << 12 | 1 << 31 from the owning lane
     uint32_t so = 0, sm = 0;
     // orientations i, i + 1 scanned together: counts (<= 49 each, <= 784 per group) in 16-bit halves
     int inclp[(NL + 1) / 2], totp[(NL + 1) / 2];
@@ -397,20 +404,20 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
         const int pos = kth_bit64(L[i], kk);
         const int W = (int)((meta[i] >> 17) & 7u);
         const int id = (int)(meta[i] & 0xFFFu) + (pos >> 3) * W + (pos & 7);
-        sel = (uint64_t)(uint32_t)id | ((uint64_t)(uint32_t)pos << 16) | (1ull << 63);
+        sel = (uint32_t)id | ((uint32_t)pos << 12) | (1u << 31);
         so = offs[i];
         sm = meta[i];
       }
       before += tot;
     }
-    sel = grp_or64<G>(sel);
+    sel = grp_or32<G>(sel);
     const uint64_t om = grp_or64<G>(((uint64_t)sm << 32) | so);
-    return Pick{(int)(sel & 0xFFFFu), (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 16) & 63u)};
+    return Pick{(int)(sel & 0xFFFu), (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 12) & 63u)};
   };
   // decode a given id -> the same Pick; id -1 when it is out of range or not a legal origin of the
   // colour whose origins L holds (the owning lane tests its bit)
   auto decode = [&](int a) {
-    uint64_t sel = 0;
+    uint32_t sel = 0;
     uint32_t so = 0, sm = 0;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
@@ -419,31 +426,22 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
       if (valid[i] && rel >= 0 && rel < (8 - h) * W) {
         const int r = (rel * (int)(meta[i] >> 23)) >> 8, c = rel - r * W;
         if ((L[i] >> (r * 8 + c)) & 1ull) {
-          sel = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)(r * 8 + c) << 16) | (1ull << 63);
+          sel = (uint32_t)a | ((uint32_t)(r * 8 + c) << 12) | (1u << 31);
           so = offs[i];
           sm = meta[i];
         }
       }
     }
-    sel = grp_or64<G>(sel);
+    sel = grp_or32<G>(sel);
     const uint64_t om = grp_or64<G>(((uint64_t)sm << 32) | so);
-    return Pick{(sel >> 63) ? (int)(sel & 0xFFFFu) : -1, (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 16) & 63u)};
+    return Pick{(sel >> 31) ? (int)(sel & 0xFFFu) : -1, (uint32_t)om, (uint32_t)(om >> 32), (int)((sel >> 12) & 63u)};
   };
-  // place pick p for colour q: cells, pieces, ply, the board hash (rows r.. r+h-1, one lane each)
+  // place pick p for colour q: cells, pieces, ply (the board hash is recomputed once at the end)
   auto place = [&](int q, const Pick& p) {
     uint64_t cells = 0;
 #pragma unroll
     for (int k = 0; k < 5; ++k) cells |= 1ull << ((p.offs >> (6 * k)) & 63u);
-    cells <<= p.org;
-    const uint64_t before = occ[q], after = before | cells;
-    const int r0 = p.org >> 3, h = (int)((p.meta >> 20) & 7u), row = r0 + j;
-    uint64_t hx = 0;
-    if (j < h) {
-      const uint32_t o = (uint32_t)(before >> (8 * row)) & 0x7Fu, nw = (uint32_t)(after >> (8 * row)) & 0x7Fu;
-      hx = (o ? row_key(q, row, o) : 0ull) ^ row_key(q, row, nw);
-    }
-    hash ^= grp_xor64<G>(hx);
-    occ[q] = after;
+    occ[q] |= cells << p.org;
     pieces[q] &= ~(1u << ((p.meta >> 12) & 31u));
     ply += 1u;
   };
@@ -501,13 +499,25 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   if (fin) {  // auto-reset (gymnasium vector-env semantics): init_state_lds's words
     occ[0] = occ[1] = 0ull;
     pieces[0] = pieces[1] = (1u << V::NP) - 1u;
-    hash = 0x9E3779B97F4A7C15ull;
     to_move = 0;
     ply = 0u;
     flags = 0u;
     last_q = -1;
   }
   if (last_q != 0) legal(0);  // the agent's legal origins for its mask
+  // the board hash (a board-only key: the seed ^ the row keys of the non-empty colour rows, as
+  // bk_vec_reset / k_next_state keep it) from the final board, one row per lane
+  uint64_t hash;
+  {
+    uint64_t hx = 0;
+#pragma unroll
+    for (int k0 = 0; k0 < 14; k0 += G) {
+      const int k = k0 + j, q = k >= 7 ? 1 : 0, row = k - 7 * q;
+      const uint32_t bits = k < 14 ? (uint32_t)(occ[q] >> (8 * row)) & 0x7Fu : 0u;
+      if (bits) hx ^= row_key(q, row, bits);
+    }
+    hash = 0x9E3779B97F4A7C15ull ^ grp_xor64<G>(hx);
+  }
   VSTAMP(4);
 
   // ---- outputs: the state words, rng, reward, done (lanes 0..3 of the env's group); obs and mask via LDS
