@@ -77,61 +77,6 @@ __global__ __launch_bounds__(256) void k_leaf_logits(DevPreset dp, DevMcts m, co
 }
 
 // grid T x 64 threads
-// The leaf logits of every tree whose leaf is to be expanded, id-stationary (the fused step's
-// alternative to each tree gathering its own W rows): workgroup w takes the ids of bitmask word w
-// (32 ids) across all trees, the (tree, id) pairs grouped by id, so a W row leaves the Infinity
-// Cache once per step for all the trees that need it and the trees' feature rows (3.2 KB each,
-// L2-resident) stream instead; each pair is row_dot16 + bias into lg_dense[t][id].
-// (tools/probe/gather.hip: the per-tree gather is bound by aggregate Infinity-Cache bandwidth.)
-// Requires F % 4 == 0 and 16-B aligned feature rows (ldf % 4 == 0).
-__global__ __launch_bounds__(256) void k_leaf_logits_ids(DevPreset dp, DevMcts m, const float* __restrict__ feat,
-                                                         int64_t ldf, int F, const float* __restrict__ W,
-                                                         const float* __restrict__ bias) {
-  __shared__ int cnt_b[32], fill_b[32], off_b[33];
-  __shared__ int pairs[256 * 32];  // (tree << 5) | bit, grouped by bit
-  const int w = blockIdx.x;
-  const int tid = threadIdx.x, l = tid & 63, wave = tid >> 6;
-  const int sub = l & 15, quad = l >> 4, F4 = F >> 2;
-  for (int t0 = 0; t0 < m.T; t0 += 256) {
-    if (tid < 32) {
-      cnt_b[tid] = 0;
-      fill_b[tid] = 0;
-    }
-    __syncthreads();
-    const int t = t0 + tid;
-    uint32_t word = 0u;
-    if (t < m.T && m.leaf_status[t] == 1)
-      word = (uint32_t)(m.leaf_mask[(size_t)t * dp.W64 + (w >> 1)] >> (32 * (w & 1)));
-    for (uint32_t b = word; b; b &= b - 1u) atomicAdd(&cnt_b[__ffs(b) - 1], 1);
-    __syncthreads();
-    if (tid == 0) {
-      int acc = 0;
-      for (int i = 0; i < 32; ++i) {
-        off_b[i] = acc;
-        acc += cnt_b[i];
-      }
-      off_b[32] = acc;
-    }
-    __syncthreads();
-    for (uint32_t b = word; b; b &= b - 1u) {
-      const int i = __ffs(b) - 1;
-      pairs[off_b[i] + atomicAdd(&fill_b[i], 1)] = (t << 5) | i;
-    }
-    __syncthreads();
-    const int np = off_b[32];
-    for (int p0 = 4 * wave; p0 < np; p0 += 16) {
-      const int p = p0 + quad;
-      const bool ok = p < np;
-      const int e = pairs[ok ? p : p0];
-      const int tt = e >> 5, id = 32 * w + (e & 31);
-      const float a = row_dot16(reinterpret_cast<const float4*>(W + (size_t)id * F),
-                                reinterpret_cast<const float4*>(feat + (size_t)tt * ldf), F4, sub);
-      if (sub == 0 && ok) m.lg_dense[(size_t)tt * dp.A + id] = a + bias[id];
-    }
-    __syncthreads();
-  }
-}
-
 __global__ __launch_bounds__(64) void k_expand_backup(DevPreset dp, DevMcts m, const float* __restrict__ logp,
                                                       const float* __restrict__ values, int prior_mode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -205,7 +150,6 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step(DevPreset dp, Dev
 // launches; what goes is the wait of the expansion and descent for the slowest logit wave.
 // lds = [W32pad mask | kLeafCap ids | F features | kLeafCap logits] then, at sel_off, the
 // descent's [state | 2 kMaxN | W32pad].
-template <bool PRE>
 __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, DevMcts m, const float* __restrict__ feat,
                                                                     int64_t ldf, int F, const float* __restrict__ W,
                                                                     const float* __restrict__ bias,
@@ -251,7 +195,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   // the value up (independent of the logits) and then waits for K to publish the new node
   int K = -1;
   if (wave > 0) {
-    K = leaf_logits_prologue_w<kStepWaves - 1, !PRE>(dp, m, t, feat, ldf, F, lds, wave, &sx, status0);
+    K = leaf_logits_prologue_w<kStepWaves - 1>(dp, m, t, feat, ldf, F, lds, wave, &sx, status0);
     if (wave == 1 && K >= 0) {
       // the new node (table entry, child range) from wave 0's loads, as soon as K is known
       wait_flag_acquire(&sx.hready);
@@ -305,12 +249,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     }
   }
   if (wave > 0 && K >= 0 && K <= kLeafCap) {
-    if (PRE) {  // the logits by id from k_leaf_logits_ids (the same dots, bitwise)
-      const float* lgd = m.lg_dense + (size_t)t * dp.A;
-      for (int j = threadIdx.x - kWave; j < K; j += kWave * (kStepWaves - 1)) lg[j] = lgd[ids[j]];
-    } else {
-      leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg);
-    }
+    leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg);
     int done = 0;
     if (lane_id() == 0) done = __hip_atomic_fetch_add(&sx.done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     done = readlane_i(done, 0);
@@ -463,8 +402,7 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
     // (node_cap grows with the simulations per move) fails here with its size, not inside hipMalloc
     const size_t C0 = (size_t)d.child_cap_per_tree * T;
     const size_t need = T * TS * sizeof(TabEntry) + C0 * (4 + 4 + 8 + 4) +
-                        T * (kMaxDepth * 12 + kStateWords * 4 + kMaxP * 8 + W64 * 8 + kLeafCap * 8 + 64 + 64 +
-                             (size_t)ctx->dp.A * 4);
+                        T * (kMaxDepth * 12 + kStateWords * 4 + kMaxP * 8 + W64 * 8 + kLeafCap * 8 + 64 + 64);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && need > free_b) {
       delete m;
@@ -494,7 +432,6 @@ int bk_mcts_create(bk_ctx* ctx, int trees, int node_cap, int64_t child_cap, bk_m
   if (!rc) rc = mcts_alloc(m, &d.leaf_ids, T * kLeafCap);
   if (!rc) rc = mcts_alloc(m, &d.leaf_logit, T * kLeafCap);
   if (!rc) rc = mcts_alloc(m, &d.leaf_K, T);
-  if (!rc) rc = mcts_alloc(m, &d.lg_dense, T * (size_t)ctx->dp.A);
   if (!rc) rc = mcts_alloc(m, &d.counters, 8);
   if (!rc) rc = hip_check(hipMemset(d.counters, 0, 8 * sizeof(unsigned long long)), "memset counters");
   if (!rc) rc = mcts_alloc(m, &d.tree_ctr, T * 8);
@@ -562,19 +499,7 @@ int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const f
   if (overlap) {
     const int sel_off = (int)(((size_t)dp.W32pad + 2 * kLeafCap + F + 3) & ~(size_t)3);
     const size_t words = (size_t)sel_off + kStateWords + 2 * kMaxN + dp.W32pad;
-    // the logits id-stationary first (BK_STEP_IDS=1), when the features allow 16-B row loads
-    const char* pe = getenv("BK_STEP_IDS");
-    const bool pre = (pe ? atoi(pe) : 0) && (F & 3) == 0 && (ldf & 3) == 0 && ((uintptr_t)feat & 15u) == 0;
-    if (pre) {
-      hipLaunchKernelGGL(k_leaf_logits_ids, dim3(dp.W32), dim3(256), 0, (hipStream_t)stream, dp, m->d, feat, ldf, F, W,
-                         bias);
-      if (int rc = launch_check("k_leaf_logits_ids")) return rc;
-      hipLaunchKernelGGL(k_leaf_step_ov<true>, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
-                         (hipStream_t)stream, dp, m->d, feat, ldf, F, W, bias, values, do_select,
-                         (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, sel_off);
-      return launch_check("k_leaf_step_ov");
-    }
-    hipLaunchKernelGGL(k_leaf_step_ov<false>, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
+    hipLaunchKernelGGL(k_leaf_step_ov, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
                        (hipStream_t)stream, dp, m->d, feat, ldf, F, W, bias, values, do_select,
                        (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, sel_off);
     return launch_check("k_leaf_step_ov");

@@ -62,7 +62,6 @@ struct DevMcts {
   uint64_t* leaf_mask;  // [T*W64] internal copy of the leaf bitmask
   int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
   float* leaf_logit;    // [T*kLeafCap] their logits
-  float* lg_dense;      // [T*A] the leaf logits by id (k_leaf_logits_ids; only the leaf's legal ids are written)
   int32_t* leaf_K;      // [T]
   unsigned long long* counters;  // [8] (errors; the totals when BK_TREE_CTR is 0)
   unsigned long long* tree_ctr;  // [T*8] per-tree counters: uncontended atomics, summed on read
@@ -434,8 +433,8 @@ __device__ __forceinline__ int leaf_logits_prologue(const DevPreset& dp, const D
 // One logit's dot product W[id] . f by the 16 lanes of a quarter wave (sub = lane & 15): a lane
 // sums every 16th float4 — whole trips of four alternate two partial sums, the rest go to the
 // first — and the 16 partial sums meet in 4 xor-shuffles. The single definition of the leaf
-// logits' arithmetic: k_leaf_logits, the fused leaf steps and k_leaf_logits_ids all sum through it,
-// so their logits agree bitwise whether f is in LDS or in global memory.
+// logits' arithmetic: k_leaf_logits and the fused leaf steps all sum through it, so their logits
+// agree bitwise.
 __device__ __forceinline__ float row_dot16(const float4* __restrict__ r, const float4* f4, int F4, int sub) {
   float a0 = 0.f, a1 = 0.f;
   int q = sub;
@@ -833,7 +832,7 @@ __device__ __forceinline__ void expand_head(const DevMcts& m, int t, const StepH
 // bitmask, offsets from the segment counts: the ids in ascending order, as compact_ids writes
 // them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32. status: the leaf status
 // the step started from (not m.leaf_status, which wave 0's next descent rewrites meanwhile).
-template <int NW, bool FEAT = true>
+template <int NW>
 __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const DevMcts& m, int t,
                                                       const float* __restrict__ feat, int64_t ldf, int F,
                                                       uint32_t* lds, int wave, StepExpand* sx, int status) {
@@ -848,10 +847,8 @@ __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const
     m32[2 * j] = (uint32_t)w;
     m32[2 * j + 1] = (uint32_t)(w >> 32);
   }
-  if (FEAT) {  // the features for the logit dots (not when the logits come precomputed)
-    const float* ft = feat + (size_t)t * ldf;
-    for (int i = tid; i < F; i += nth) f[i] = ft[i];
-  }
+  const float* ft = feat + (size_t)t * ldf;
+  for (int i = tid; i < F; i += nth) f[i] = ft[i];
   auto arrive_wait = [&](int* ctr) {  // a barrier of the NW logit waves (LDS counter)
     if (l == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NW) __builtin_amdgcn_s_sleep(1);
