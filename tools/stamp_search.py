@@ -1,6 +1,7 @@
 """Diagnostic: per-phase cycle shares of k_select / k_expand_backup from the BK_STAMPS build
 (BK_LIB=blokus_rl_amd/_lib/diag/libblokus_hip_diag.so). Runs self-play plies with the bench's
-ResNet leaf net (or, with --dumbnet, the uninformed search), then stamps 30 simulations."""
+ResNet leaf net (or, with --dumbnet, the uninformed search), then stamps 30 simulations.
+Usage: python tools/stamp_search.py [plies (4)] [--dumbnet]"""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -13,7 +14,8 @@ eng = Engine(20, 4, 5)
 torch.manual_seed(0)
 net = DumbNet(20, 4, eng.A) if "--dumbnet" in sys.argv else build_model("resnet", 20, 4, eng.A, num_res_blocks=5)
 sp = SelfPlay(eng, net.to(eng.device).eval(), 256, num_sims=100, seed=1234, continuous=True)
-for _ in range(4):
+plies = int(next((a for a in sys.argv[1:] if a.isdigit()), "4"))
+for _ in range(plies):
     sp.play_ply()
 lib = engine.load_library()
 lib.bk_debug_stamps.argtypes = [ctypes.c_void_p]
