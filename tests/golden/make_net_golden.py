@@ -7,7 +7,8 @@ package modules they import but do not need for a forward pass (blokus_rl.coloss
 blokus_rl.utils) stubbed, fills every parameter/buffer deterministically by name
 (`det_state_dict`, shared with the tests, so no weights are stored), and records on CPU:
   * 7x7 2-player (A=2522) ResNet(2 blocks) and DCNNet: full log-prob rows and values;
-  * 20x20 4-player (A=30433) ResNet(2 blocks): predict(obs, mask) -> (p over legal ids, v).
+  * 20x20 4-player (A=30433) ResNet(2 and 5 blocks): predict(obs, mask) -> (p over legal ids, v)
+    on 3 mid-game boards, the empty board and up to 8 boards spread over a game.
 Observations/masks come from oracle random boards. Output: tests/golden/net_golden.npz.
 """
 import importlib.util
@@ -135,7 +136,10 @@ def main():
     out["obs7"] = obs7
     # 20x20: the reference predict() path
     o20 = Oracle(20, 4, 5)
-    boards20 = [o20.random_board(s, 40) for s in (1, 2, 3)]
+    # three mid-game boards (the round-1 rows), the empty board (first move) and boards spread over
+    # a whole game (seeds 4..11, up to 80 random plies; a mover without a legal move is skipped)
+    boards20 = [o20.random_board(s, 40) for s in (1, 2, 3)] + [o20.init_state()]
+    boards20 += [b for b in (o20.random_board(s, 80) for s in range(4, 12)) if len(o20.legal_ids(b)) > 0]
     hp20 = _HP(num_res_blocks=2, num_channels=128, linear_dim=128, dropout=0.3, lr=1e-3, weight_decay=1e-4,
                model_type="resnet")
     g20 = _Game(20, 4, o20.A)
