@@ -643,6 +643,8 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--late-plies", type=int, default=30,
+                    help="self-play: plies timed after the window (the late game; 0 = skip), sub-field late_game")
     ap.add_argument("--games", type=int, default=256)
     ap.add_argument("--sims", type=int, default=100)
     ap.add_argument("--model", default="resnet", choices=["resnet", "dumbnet", "dcnnet"])

@@ -130,6 +130,29 @@ def run_selfplay(model_type: str, nn_dtype: str, G: int, sims: int, steps: int, 
     return sp, eng, done, elapsed, delta, ms
 
 
+def late_game(sp, plies: int, done: int) -> dict:
+    """After the timed window (and the stage-timed ply): `plies` more plies of the same run,
+    timed (sims/s and ms per ply of this rank; games that end restart, as in the window), then the
+    live leaf-step time there — the window covers plies 5-30 of a ~60-80-ply game, this the rest
+    (SURVEY §8d asks for the whole game's plies). {} when plies <= 0."""
+    if plies <= 0:
+        return {}
+    torch.cuda.synchronize()
+    sims0 = sp.stats.sims
+    t0 = time.perf_counter()
+    for _ in range(plies):
+        sp.play_ply()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    sp.check()
+    out = {"plies": f"{done + 1}-{done + plies}", "sims_per_s": (sp.stats.sims - sims0) / dt,
+           "ms_per_ply": dt / plies * 1e3}
+    ls = time_leaf_step(sp)
+    if ls is not None:
+        out["k_leaf_step_us"] = ls["k_leaf_step_us"]
+    return out
+
+
 def stage_times(sp) -> dict:
     """Stage times outside the timed region: one ply launched stage by stage with events around
     each stage: select / net / expand ms per sim-step."""
@@ -267,6 +290,7 @@ def bench_selfplay(args, world, rank):
         search = {"bound": "hbm", "kernel": "k_select+k_expand_backup (search, stage-timed eager ply)",
                   "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
                   "traffic": None, "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms}
+    late = late_game(sp, getattr(args, "late_plies", 0), args.warmup + args.steps + 1)
     ks = ms.pop("k_sims", None)
     out = {
         "metric": "MCTS sims/sec on 20x20 Blokus (4 players, 256 games/GPU, 100 sims/move)",
@@ -288,6 +312,8 @@ def bench_selfplay(args, world, rank):
         "stage_ms_per_sim_step": ms,
         "engine_counters": delta,
     }
+    if late:
+        out["late_game"] = late
     if conv is not None:
         cms, cflop, dflop, cpeak = conv["ms"], conv["flop"], conv["direct"], conv["peak"]
         out["tower_roofline"] = {"bound": "mfma", "kernel": conv["kernel"],
