@@ -19,7 +19,7 @@
 #define BK_BOARD_SYNC() ::bk::wave_lds_sync()
 #ifdef BK_STAMPS
 #include <hip/hip_runtime.h>
-static __device__ unsigned long long g_step_stamps[4096][8];  // diag: k_leaf_step phase stamps
+static __device__ unsigned long long g_step_stamps[4096][16];  // diag: k_leaf_step phase stamps
 // diag: phases inside the leaf bitmask build of k_leaf_step (slots 5..7), thread 0 of the group
 #define BK_MASK_STAMP(i) \
   do { if (threadIdx.x == 0 && blockIdx.x < 4096 && blockDim.x > 256) g_step_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -166,7 +166,8 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #ifdef BK_STAMPS
   // diag: 0 start, 1 the new node's entry published (wave 1), 2 wave 0 backup done, 3 wave 0 descent done, 4 the last logit
-  // wave done, 5 its children stored, 6 the next leaf's bitmask done (all waves), 7 end
+  // wave done, 5 its children stored, 6 the next leaf's bitmask done (all waves), 7 end, 8 wave 0 out of the
+  // bitmask claims (select_leaf's own stamps: g_stamps[0][t][4] stores issued, [5] observation issued)
 #define BK_OV_STAMP(i) \
   do { if (lane_id() == 0 && do_select && t < 4096) g_step_stamps[t][i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -270,6 +271,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     while (__hip_atomic_load(&sx.leaf_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
       __builtin_amdgcn_s_sleep(1);
     if (readlane_i(status_sh, 0) == 1) mask_slices_claim(dp, lsel, m32, &sx.slice);
+    if (wave == 0) BK_OV_STAMP(8);  // wave 0 has no slice left to claim
   }
   __syncthreads();
   if (wave == 0) BK_OV_STAMP(6);
@@ -375,7 +377,7 @@ extern "C" {
 int bk_debug_stamps(unsigned long long* out) {  // [2][4096][8] host copy
   return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)), "stamps");
 }
-int bk_debug_step_stamps(unsigned long long* out) {  // [4096][8] host copy: k_leaf_step phases
+int bk_debug_step_stamps(unsigned long long* out) {  // [4096][16] host copy: k_leaf_step phases
   return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamps), sizeof(g_step_stamps)), "step stamps");
 }
 #endif

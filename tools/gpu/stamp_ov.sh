@@ -5,5 +5,5 @@ out=gpurun_out/stamp_ov
 mkdir -p $out
 for p in 6 15 25; do
   BK_LIB=blokus_rl_amd/_lib/diag/libblokus_hip_diag.so timeout -k 10 200 python tools/stamp_step_ov.py $p > $out/ply$p.json 2> $out/ply$p.err || { tail $out/ply$p.err; exit 1; }
-  echo "ply $p"; cut -c1-900 $out/ply$p.json
+  echo "ply $p"; cut -c1-4000 $out/ply$p.json
 done

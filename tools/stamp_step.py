@@ -18,7 +18,7 @@ for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
 torch.cuda.synchronize()
 lib = engine.load_library()
 lib.bk_debug_step_stamps.argtypes = [ctypes.c_void_p]
-buf = np.zeros((4096, 8), dtype=np.uint64)
+buf = np.zeros((4096, 16), dtype=np.uint64)
 assert lib.bk_debug_step_stamps(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 a = buf[:256, :5].astype(np.int64)  # the last k_leaf_step launch
 d = np.diff(a, axis=1)

@@ -24,11 +24,15 @@ for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
 torch.cuda.synchronize()
 lib = engine.load_library()
 lib.bk_debug_step_stamps.argtypes = [ctypes.c_void_p]
-buf = np.zeros((4096, 8), dtype=np.uint64)
+buf = np.zeros((4096, 16), dtype=np.uint64)
 assert lib.bk_debug_step_stamps(buf.ctypes.data_as(ctypes.c_void_p)) == 0
+lib.bk_debug_stamps.argtypes = [ctypes.c_void_p]
+sb = np.zeros((2, 4096, 8), dtype=np.uint64)
+assert lib.bk_debug_stamps(sb.ctypes.data_as(ctypes.c_void_p)) == 0
 a = buf[:256].astype(np.int64)
+g0, g1 = sb[0, :256].astype(np.int64), sb[1, :256].astype(np.int64)
 ok = (a[:, 7] > 0) & (a[:, 4] > 0)
-a = a[ok]
+a, g0, g1 = a[ok], g0[ok], g1[ok]
 rel = a - a[:, :1]
 names = ["node added (wave 1)", "wave0 backup", "wave0 descent", "logits (last wave)", "children", "mask done", "obs/end"]
 out = {"trees": int(ok.sum()), "total_median": float(np.median(rel[:, 7])), "total_max": float(rel[:, 7].max()),
@@ -36,6 +40,11 @@ out = {"trees": int(ok.sum()), "total_median": float(np.median(rel[:, 7])), "tot
 for i, nm in zip([1, 2, 3, 4, 5, 6, 7], names):
     out[nm] = {"median": float(np.median(rel[:, i])), "p90": float(np.percentile(rel[:, i], 90)),
                "max": float(rel[:, i].max())}
+extra = {"wave0 out of mask claims": a[:, 8] - a[:, 0], "select_leaf stores issued": g0[:, 4] - a[:, 0],
+         "select_leaf obs issued": g0[:, 5] - a[:, 0], "descent probe (sum)": g0[:, 6], "descent PUCT scan (sum)": g0[:, 7],
+         "descent placement (sum)": g1[:, 7], "descent next-mover check (sum)": g1[:, 6]}
+for nm, v in extra.items():
+    out[nm] = {"median": float(np.median(v)), "p90": float(np.percentile(v, 90)), "max": float(v.max())}
 slow = np.argsort(rel[:, 7])[-10:]
 out["slowest10"] = [[int(x) for x in rel[j, 1:]] for j in slow]
 K = sp.mcts.__dict__.get("_k", None)
