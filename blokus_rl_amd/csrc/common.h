@@ -23,7 +23,7 @@ struct DevPreset {
   int8_t corner_r[kMaxP], corner_c[kMaxP];
   int16_t piece_item_off[kNumPieces + 1];
   const uint64_t* items;  // [num_items]
-  const uint32_t* act;    // [A]
+  const uint4* act_it;    // [A]: the action's item (lo, hi words) and its act word (item | col << 16 | piece << 24)
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
@@ -244,8 +244,11 @@ __device__ __forceinline__ int place_action(const DevPreset& dp, uint32_t* s, in
   const int l = lane_id();
   const int p = (int)s[kWToMove];
   if (a < 0 || a >= dp.A) return 1;
-  const uint32_t ad = dp.act[a];
-  const uint64_t it = dp.items[ad & 0xFFFFu];
+  // one 16-B load (the act word and its item together: the descent's placement was two dependent
+  // round trips per level, queued behind the policy-row gather of the fused step)
+  const uint4 e = dp.act_it[a];
+  const uint32_t ad = e.z;
+  const uint64_t it = (uint64_t)e.x | ((uint64_t)e.y << 32);
   const int c = (int)((ad >> 16) & 0xFFu);
   const int pc = (int)(ad >> 24);
   if (VALIDATE) {

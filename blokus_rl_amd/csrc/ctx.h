@@ -12,7 +12,7 @@ struct bk_ctx {
   bk::DevPreset dp;
   int device = 0;
   uint64_t* d_items = nullptr;
-  uint32_t* d_act = nullptr;
+  uint4* d_act_it = nullptr;  // [A] item + act word per action (place_action)
   uint32_t* d_pack = nullptr;       // [W64] x 4: k_legal_mask_staged's word assembly table
   bool legal_items_kernel = false;  // BK_LEGAL_KERNEL=items selects the item-loop kernel (A/B)
   int legal_wpb = 1;                // BK_LEGAL_WPB: variant of k_legal_mask_rows (A/B knob)

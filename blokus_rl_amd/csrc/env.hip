@@ -222,11 +222,16 @@ int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int devi
   int rc = hip_check(hipSetDevice(device), "hipSetDevice");
   if (rc) { delete c; return rc; }
   rc = hip_check(hipMalloc(&c->d_items, sizeof(uint64_t) * p.items.size()), "hipMalloc items");
-  if (!rc) rc = hip_check(hipMalloc(&c->d_act, sizeof(uint32_t) * p.act.size()), "hipMalloc act");
+  std::vector<uint4> act_it(p.act.size());
+  for (size_t a = 0; a < p.act.size(); ++a) {
+    const uint64_t it = p.items[p.act[a] & 0xFFFFu];
+    act_it[a] = make_uint4((uint32_t)it, (uint32_t)(it >> 32), p.act[a], 0u);
+  }
+  if (!rc) rc = hip_check(hipMalloc(&c->d_act_it, sizeof(uint4) * act_it.size()), "hipMalloc act_it");
   if (!rc) rc = hip_check(hipMemcpy(c->d_items, p.items.data(), sizeof(uint64_t) * p.items.size(),
                                     hipMemcpyHostToDevice), "copy items");
-  if (!rc) rc = hip_check(hipMemcpy(c->d_act, p.act.data(), sizeof(uint32_t) * p.act.size(),
-                                    hipMemcpyHostToDevice), "copy act");
+  if (!rc) rc = hip_check(hipMemcpy(c->d_act_it, act_it.data(), sizeof(uint4) * act_it.size(),
+                                    hipMemcpyHostToDevice), "copy act_it");
   if (!rc) {
     // k_legal_mask_staged's pack table: u32 word k of the mask is the OR over the fields
     // overlapping it of hi32(field << sh), field (O, r) at stage slot O * kStageRows + r starting
@@ -262,7 +267,7 @@ int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int devi
   }
   if (rc) { bk_ctx_destroy(c); return rc; }
   d.items = c->d_items;
-  d.act = c->d_act;
+  d.act_it = c->d_act_it;
   *out = c;
   return BK_OK;
 }
@@ -270,7 +275,7 @@ int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int devi
 int bk_ctx_destroy(bk_ctx* c) {
   if (!c) return BK_OK;
   if (c->d_items) (void)hipFree(c->d_items);
-  if (c->d_act) (void)hipFree(c->d_act);
+  if (c->d_act_it) (void)hipFree(c->d_act_it);
   if (c->d_pack) (void)hipFree(c->d_pack);
   delete c;
   return BK_OK;

@@ -241,6 +241,11 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
   double cp = cpuct, eps = root_eps;
   int depth = 0, err = 0;
   long long scanned = 0;
+  // the path records of levels 0..63 stay in lane `level`'s registers until the descent ends: a
+  // store per level would make every next level's first load wait for it (vmcnt counts stores too),
+  // and under the fused step's gather a store takes as long as a round trip to be acknowledged
+  int64_t rec_child = 0;
+  int rec_pl = 0;
 #ifdef BK_STAMPS
   unsigned long long t_probe = 0, t_child = 0, t_apply = 0, t_adv = 0;
 #define BK_TACC(v, stmt)                                         \
@@ -283,7 +288,12 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     BK_TACC(t_apply, bad = place_action<false>(dp, s, a, fa));
     BK_TACC(t_adv, if (!bad) advance_turn(dp, s, p, [&](int q) { return rows_any_legal(dp, s, q); }));
     if (bad) { err |= kErrIllegal; break; }
-    if (l == 0) {
+    if (depth < kWave) {
+      if (l == depth) {
+        rec_child = off + ci;
+        rec_pl = (int)s[kWToMove];
+      }
+    } else if (l == 0) {  // levels 64..kMaxDepth-1 (never at 20x20)
       const size_t pi = (size_t)t * kMaxDepth + depth;
       m.path_child[pi] = off + ci;
       m.path_pl[pi] = (int)s[kWToMove];
@@ -291,6 +301,11 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
     ++depth;
     cp = 1.0;    // the recursive call of mcts.py:50 passes no cpuct
     eps = 1e-6;  // nor epsilon_fix (its default True)
+  }
+  if (l < depth && l < kWave) {
+    const size_t pi = (size_t)t * kMaxDepth + l;
+    m.path_child[pi] = rec_child;
+    m.path_pl[pi] = rec_pl;
   }
   BK_STAMP(0, 2);
 #ifdef BK_STAMPS
