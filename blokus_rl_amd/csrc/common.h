@@ -20,7 +20,11 @@ struct DevPreset {
   int N, P, A, W64, W32, W32pad, num_items, num_pieces;
   uint32_t full_pieces;
   uint32_t full_row;  // (1 << N) - 1
-  int8_t corner_r[kMaxP], corner_c[kMaxP];
+  // the start corners, one byte per colour: an index by the (runtime) colour is a shift of a kernel
+  // argument held in SGPRs, not a byte load from the kernarg segment (a memory round trip per use)
+  uint32_t corner_r4, corner_c4;
+  __device__ __forceinline__ int corner_r(int q) const { return (int)((corner_r4 >> (8 * q)) & 0xFFu); }
+  __device__ __forceinline__ int corner_c(int q) const { return (int)((corner_c4 >> (8 * q)) & 0xFFu); }
   int16_t piece_item_off[kNumPieces + 1];
   const uint64_t* items;  // [num_items]
   const uint4* act_it;    // [A]: the action's item (lo, hi words) and its act word (item | col << 16 | piece << 24)
@@ -151,7 +155,7 @@ __device__ __forceinline__ bool compute_fa(const DevPreset& dp, const uint32_t* 
   if (l < N) {
     forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
     if (first)
-      anch = (l == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+      anch = (l == dp.corner_r(q)) ? (1u << dp.corner_c(q)) : 0u;
     else
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
     fa[l] = (uint64_t)forb | ((uint64_t)anch << 32);
@@ -246,7 +250,8 @@ __device__ __forceinline__ int place_action(const DevPreset& dp, uint32_t* s, in
   if (a < 0 || a >= dp.A) return 1;
   // one 16-B load (the act word and its item together: the descent's placement was two dependent
   // round trips per level, queued behind the policy-row gather of the fused step)
-  const uint4 e = dp.act_it[a];
+  uint4 e = dp.act_it[a];
+  asm volatile("" : "+v"(e.x), "+v"(e.y), "+v"(e.z), "+v"(e.w));  // one load (not the word, then the item)
   const uint32_t ad = e.z;
   const uint64_t it = (uint64_t)e.x | ((uint64_t)e.y << 32);
   const int c = (int)((ad >> 16) & 0xFFu);

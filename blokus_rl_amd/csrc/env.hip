@@ -194,7 +194,11 @@ int bk_ctx_create(int board_size, int num_players, int max_piece_cells, int devi
   d.num_items = p.num_items; d.num_pieces = p.num_pieces;
   d.full_pieces = p.full_pieces;
   d.full_row = (1u << p.N) - 1u;
-  for (int k = 0; k < kMaxP; ++k) { d.corner_r[k] = (int8_t)p.corner_r[k]; d.corner_c[k] = (int8_t)p.corner_c[k]; }
+  d.corner_r4 = d.corner_c4 = 0u;
+  for (int k = 0; k < kMaxP; ++k) {
+    d.corner_r4 |= (uint32_t)(p.corner_r[k] & 0xFF) << (8 * k);
+    d.corner_c4 |= (uint32_t)(p.corner_c[k] & 0xFF) << (8 * k);
+  }
   for (int i = 0; i <= kNumPieces; ++i) d.piece_item_off[i] = (int16_t)p.piece_item_off[i];
   // the unrolled kernel's compile-time orientations must be the host tables' orientations
   bool same = (int)p.orients.size() <= kNumOrient;

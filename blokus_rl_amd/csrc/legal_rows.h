@@ -156,7 +156,7 @@ __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s
   if (ok) {
     forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
     if (first)
-      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+      anch = (r == dp.corner_r(q)) ? (1u << dp.corner_c(q)) : 0u;
     else
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
@@ -251,7 +251,7 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
   if (ok) {
     forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
     if (first)
-      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+      anch = (r == dp.corner_r(q)) ? (1u << dp.corner_c(q)) : 0u;
     else
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   if (ok) {
     forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
     if (first)
-      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+      anch = (r == dp.corner_r(q)) ? (1u << dp.corner_c(q)) : 0u;
     else
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(64) void k_legal_mask_staged(DevPreset dp, const ui
   if (ok) {
     forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
     if (first)
-      anch = (r == dp.corner_r[q]) ? (1u << dp.corner_c[q]) : 0u;
+      anch = (r == dp.corner_r(q)) ? (1u << dp.corner_c(q)) : 0u;
     else
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
