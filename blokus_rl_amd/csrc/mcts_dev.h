@@ -99,7 +99,14 @@ __device__ __forceinline__ bool table_find(const DevMcts& m, int t, uint64_t key
   const TabEntry* tab = m.tab + (size_t)t * m.TS;
   for (int p0 = 0; p0 < m.TS; p0 += kWave) {
     const uint32_t slot = (start + (uint32_t)(p0 + l)) & mask;
-    const TabEntry e = tab[slot];
+    // the whole 16-B entry in one load: left alone the compiler loads the key, compares, and only
+    // then loads (off, K) in the hit branch — a second dependent round trip per probe
+    uint4 ev = *reinterpret_cast<const uint4*>(tab + slot);
+    asm volatile("" : "+v"(ev.x), "+v"(ev.y), "+v"(ev.z), "+v"(ev.w));
+    TabEntry e;
+    e.key = (unsigned long long)ev.x | ((unsigned long long)ev.y << 32);
+    e.off = ev.z;
+    e.K = (int32_t)ev.w;
     const uint64_t hit = __ballot(e.key == key);
     const uint64_t emp = __ballot(e.key == 0ull);
     if (hit) {
