@@ -191,13 +191,17 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
     status0_sh = m.leaf_status[t];
   }
   if (wave == 0) BK_OV_STAMP(0);
+  // the logit waves' bitmask words and features in flight across the barrier (read whatever the
+  // status; used only when it is 1)
+  LeafPre pre{0ull, 0.0f, false};
+  if (wave > 0) pre = leaf_pre_load<kStepWaves - 1>(dp, m, t, feat, ldf, F);
   __syncthreads();
   const int status0 = status0_sh;
   // waves 1..: the logit prologue (legal ids compacted, features in LDS); wave 0 meanwhile backs
   // the value up (independent of the logits) and then waits for K to publish the new node
   int K = -1;
   if (wave > 0) {
-    K = leaf_logits_prologue_w<kStepWaves - 1>(dp, m, t, feat, ldf, F, lds, wave, &sx, status0);
+    K = leaf_logits_prologue_w<kStepWaves - 1>(dp, m, t, feat, ldf, F, lds, wave, &sx, status0, &pre);
     if (wave == 1 && K >= 0) {
       // the new node (table entry, child range) from wave 0's loads, as soon as K is known
       wait_flag_acquire(&sx.hready);
@@ -251,6 +255,9 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
         __hip_atomic_store(&sx.leaf_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       BK_OV_STAMP(3);
+      // the next leaf's observation rows and state now, while the logit waves are busy (they were
+      // the step's tail, after the bitmask)
+      leaf_obs_rows<1>(dp, m, t, st, obs, lsel, lane_id());
     }
     if (prio) __builtin_amdgcn_s_setprio(0);
   }
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   __syncthreads();
   if (wave == 0) BK_OV_STAMP(6);
   if (!do_select) return;
-  select_leaf<kStepWaves, true>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
+  select_leaf<kStepWaves, true, false>(dp, m, t, status_sh, obs, mask_out, lsel, wave);
   if (wave == 0) BK_OV_STAMP(7);
 #undef BK_OV_STAMP
 }

@@ -345,12 +345,39 @@ __device__ __forceinline__ int select_descend(const DevPreset& dp, const DevMcts
   return status;
 }
 
+// The observation rows of tree t's leaf (state s in LDS) and its state, by NW waves (thread tid of
+// NW * 64): zeros unless status 1. select_leaf's rows, callable on their own.
+template <int NW>
+__device__ __forceinline__ void leaf_obs_rows(const DevPreset& dp, const DevMcts& m, int t, int status,
+                                              float* __restrict__ obs, const uint32_t* s, int tid) {
+  if (status == 1 && tid < kWave) store_state(m.leaf_state + (size_t)t * kStateWords, s);
+  const int obs_len = 2 * dp.P * dp.N * dp.N;
+  float* o = obs ? obs + (size_t)t * obs_len : nullptr;
+  const int tm = (int)s[kWToMove];
+  const int rows = 2 * dp.P * dp.N;
+  for (int pr = tid; o && pr < rows; pr += NW * kWave) {
+    const int plane = pr / dp.N, r = pr - plane * dp.N;
+    uint32_t bits = 0u;
+    if (status == 1) bits = plane < dp.P ? s[plane * kMaxN + r] : ((plane - dp.P) == tm ? dp.full_row : 0u);
+    float* dst = o + pr * dp.N;
+    if ((dp.N & 3) == 0) {
+      for (int c = 0; c < dp.N; c += 4)
+        *reinterpret_cast<float4*>(dst + c) = make_float4((float)((bits >> c) & 1u), (float)((bits >> (c + 1)) & 1u),
+                                                          (float)((bits >> (c + 2)) & 1u), (float)((bits >> (c + 3)) & 1u));
+    } else {
+      for (int c = 0; c < dp.N; ++c) dst[c] = (float)((bits >> c) & 1u);
+    }
+  }
+}
+
 // The leaf of a descent (state in LDS), by the NW waves of the workgroup (wave = this one's
 // index; 1 = the descending wave alone): for a leaf (status 1) the mover's legal bitmask (the
 // orientations split over the waves) and the leaf state to global memory, and for every tree
 // the observation rows the net reads (zeros unless status 1). obs and mask_out may be null.
 // BUILT: the bitmask is already in LDS (k_leaf_step_ov builds it with mask_slices_claim).
-template <int NW, bool BUILT = false>
+// OBS: write the observation rows here (k_leaf_step_ov's descending wave writes them itself, with
+// leaf_obs_rows, while the other waves still compute logits).
+template <int NW, bool BUILT = false, bool OBS = true>
 __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& m, int t, int status,
                                             float* __restrict__ obs, uint64_t* __restrict__ mask_out, uint32_t* lds,
                                             int wave) {
@@ -373,9 +400,10 @@ __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& 
       mo[j] = w;
       if (mo2) mo2[j] = w;
     }
-    if (wave == 0) store_state(m.leaf_state + (size_t)t * kStateWords, s);
+    if (wave == 0 && OBS) store_state(m.leaf_state + (size_t)t * kStateWords, s);
   }
   BK_STAMP(0, 4);
+  if (!OBS) return;
   // observation row (zeros unless the leaf needs the net): thread = (plane, board row), the row's
   // N floats as float4 stores when N is a multiple of 4 (no per-cell index arithmetic)
   float* o = obs ? obs + (size_t)t * obs_len : nullptr;
@@ -854,23 +882,50 @@ __device__ __forceinline__ void expand_head(const DevMcts& m, int t, const StepH
 // bitmask, offsets from the segment counts: the ids in ascending order, as compact_ids writes
 // them). Wave 1 publishes K (sx->kready) and leaf_K. Needs NW * 64 >= W32. status: the leaf status
 // the step started from (not m.leaf_status, which wave 0's next descent rewrites meanwhile).
+// pre (optional): this thread's word of the leaf bitmask and its feature, loaded before the
+// step's first barrier (ok when one of each per thread covers them), so the prologue does not start
+// with a round trip of its own after the status is known.
+struct LeafPre {
+  uint64_t w;
+  float f;
+  bool ok;
+};
+template <int NW>
+__device__ __forceinline__ LeafPre leaf_pre_load(const DevPreset& dp, const DevMcts& m, int t,
+                                                 const float* __restrict__ feat, int64_t ldf, int F) {
+  const int tid = threadIdx.x - kWave, nth = NW * kWave;
+  LeafPre p;
+  p.ok = dp.W64 <= nth && F <= nth;
+  p.w = p.ok && tid < dp.W64 ? m.leaf_mask[(size_t)t * dp.W64 + tid] : 0ull;
+  p.f = p.ok && tid < F ? feat[(size_t)t * ldf + tid] : 0.0f;
+  return p;
+}
 template <int NW>
 __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const DevMcts& m, int t,
                                                       const float* __restrict__ feat, int64_t ldf, int F,
-                                                      uint32_t* lds, int wave, StepExpand* sx, int status) {
+                                                      uint32_t* lds, int wave, StepExpand* sx, int status,
+                                                      const LeafPre* pre = nullptr) {
   uint32_t* m32 = lds;
   int32_t* ids = reinterpret_cast<int32_t*>(lds + dp.W32pad);
   float* f = reinterpret_cast<float*>(lds + dp.W32pad + kLeafCap);
   if (status != 1) return -1;  // uniform over these waves: no leaf to evaluate
   const int tid = threadIdx.x - kWave, nth = NW * kWave, l = lane_id();
-  const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
-  for (int j = tid; j < dp.W64; j += nth) {
-    const uint64_t w = lm[j];
-    m32[2 * j] = (uint32_t)w;
-    m32[2 * j + 1] = (uint32_t)(w >> 32);
+  if (pre && pre->ok) {
+    if (tid < dp.W64) {
+      m32[2 * tid] = (uint32_t)pre->w;
+      m32[2 * tid + 1] = (uint32_t)(pre->w >> 32);
+    }
+    if (tid < F) f[tid] = pre->f;
+  } else {
+    const uint64_t* lm = m.leaf_mask + (size_t)t * dp.W64;
+    for (int j = tid; j < dp.W64; j += nth) {
+      const uint64_t w = lm[j];
+      m32[2 * j] = (uint32_t)w;
+      m32[2 * j + 1] = (uint32_t)(w >> 32);
+    }
+    const float* ft = feat + (size_t)t * ldf;
+    for (int i = tid; i < F; i += nth) f[i] = ft[i];
   }
-  const float* ft = feat + (size_t)t * ldf;
-  for (int i = tid; i < F; i += nth) f[i] = ft[i];
   auto arrive_wait = [&](int* ctr) {  // a barrier of the NW logit waves (LDS counter)
     if (l == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NW) __builtin_amdgcn_s_sleep(1);
