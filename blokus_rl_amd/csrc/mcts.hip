@@ -272,8 +272,17 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
         __builtin_amdgcn_s_sleep(1);
       const int err = readlane_i(sx.err, 0);
       if (err == 0) expand_children_lds(m, (int64_t)sx.off, K, ids, lg);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the children stored before the flag
-      if (lane_id() == 0) __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // the flag orders the children before the descent's reads of them; once the descent is over
+      // nobody reads them in this launch, so the stores drain under the bitmask instead of being
+      // waited for here (the kernel's end orders them for the next launch)
+      const bool descended = readlane_i(__hip_atomic_load(&sx.leaf_ready, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP), 0) != 0;
+      if (!descended) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the children stored before the flag
+        if (lane_id() == 0) __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (lane_id() == 0) {
+        __hip_atomic_store(&sx.pready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       BK_OV_STAMP(5);
     }
   }
