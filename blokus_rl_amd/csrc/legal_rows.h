@@ -16,6 +16,8 @@
 
 namespace bk {
 
+__device__ const int kNoPlayer = -1;  // k_legal_mask_rows: the player read when none is given
+
 struct RowCtx {
   uint32_t fr[5];      // bit-reversed forbidden rows r..r+4
   uint32_t ar[5];      // bit-reversed anchor rows r..r+4
@@ -310,8 +312,13 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     o3 = s[3 * kMaxN + r];
 #pragma unroll
     for (int k = 0; k < kMaxP; ++k) pieces4[k] = s[kWPieces + k];
-    q = players ? players[b] : -1;
-    if (q < 0) q = (int)s[kWToMove];
+    // the state's mover and the given player both read unconditionally with the rest (a null
+    // `players` reads a -1 constant): read only when players[b] < 0, the mover was a second round
+    // trip after the rows, and one wave's latency is the launch at the config's batch
+    const int* pp = players ? players + b : &kNoPlayer;
+    const int pq = *pp;
+    const uint32_t tm = s[kWToMove];
+    q = pq < 0 ? (int)tm : pq;
   }
   const uint32_t own = q == 0 ? o0 : q == 1 ? o1 : q == 2 ? o2 : o3;
   const uint32_t pieces = q == 0 ? pieces4[0] : q == 1 ? pieces4[1] : q == 2 ? pieces4[2] : pieces4[3];
