@@ -393,13 +393,16 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // v = tanh(W2 relu(W1 vfeat + b1) + b2); the 4 waves sweep quarters of W1's inputs
   float* vfeat = hp + NN * 12;
   float* part = vfeat + NN;
+  // the head biases in registers first: read inside the loop, each was re-loaded after every pf
+  // store (the compiler cannot rule out aliasing), one dependent round trip per store
+  const float bp0 = hd.bp[0], bp1 = hd.bp[1], bv0 = hd.bv[0];
   for (int i = tid; i < NN; i += kLnThreads) {
     const float* q = hp + i * 12;
     const float p0 = ((q[0] + q[3]) + q[6]) + q[9], p1 = ((q[1] + q[4]) + q[7]) + q[10],
                 pv = ((q[2] + q[5]) + q[8]) + q[11];
-    hd.pf[b * 2 * NN + i] = fmaxf(p0 + hd.bp[0], 0.0f);
-    hd.pf[b * 2 * NN + NN + i] = fmaxf(p1 + hd.bp[1], 0.0f);
-    vfeat[i] = fmaxf(pv + hd.bv[0], 0.0f);
+    hd.pf[b * 2 * NN + i] = fmaxf(p0 + bp0, 0.0f);
+    hd.pf[b * 2 * NN + NN + i] = fmaxf(p1 + bp1, 0.0f);
+    vfeat[i] = fmaxf(pv + bv0, 0.0f);
   }
   __syncthreads();
   {
@@ -426,10 +429,20 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   }
   __syncthreads();
   if (wave == 0) {
+    // W2 rows and b2 loaded together before the value stores (same aliasing as above)
+    float w2[kMaxP], b2[kMaxP];
+#pragma unroll
+    for (int q = 0; q < kMaxP; ++q) {
+      w2[q] = q < hd.P ? hd.w2[q * 64 + l] : 0.0f;
+      b2[q] = q < hd.P ? hd.b2[q] : 0.0f;
+    }
     const float h = fmaxf(((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) + hd.b1[l], 0.0f);
-    for (int q = 0; q < hd.P; ++q) {
-      const float sum = wave_sum_f(hd.w2[q * 64 + l] * h);
-      if (l == 0) hd.v[b * hd.P + q] = tanhf(sum + hd.b2[q]);
+#pragma unroll
+    for (int q = 0; q < kMaxP; ++q) {
+      if (q < hd.P) {
+        const float sum = wave_sum_f(w2[q] * h);
+        if (l == 0) hd.v[b * hd.P + q] = tanhf(sum + b2[q]);
+      }
     }
   }
   LNSTAMP(29, __builtin_amdgcn_s_memtime());
