@@ -485,19 +485,53 @@ __device__ __forceinline__ int leaf_logits_prologue(const DevPreset& dp, const D
 // first — and the 16 partial sums meet in 4 xor-shuffles. The single definition of the leaf
 // logits' arithmetic: k_leaf_logits and the fused leaf steps all sum through it, so their logits
 // agree bitwise.
-__device__ __forceinline__ float row_dot16(const float4* __restrict__ r, const float4* f4, int F4, int sub) {
+// SKIP: a W float4 is loaded only where the lane's four features are not all zero (the policy
+// features are a ReLU's output: ~half of them, a third of whole 128-B lines, are zero); a skipped
+// float4 enters the sum as 0 . 0 = +0, exactly what 0 . w would add (a sum that starts at +0 never
+// becomes -0, and +-0 leaves a non-zero sum unchanged), so the logits are bitwise those without the
+// skip for finite weights — and the skipped lines never leave the Infinity Cache.
+// The skipped loads are raw buffer loads at an out-of-range offset (the hardware's range check
+// returns zeros without a memory access), so the four loads of a trip stay branch-free and in
+// flight together (exec-masked branches made the compiler wait for each).
+__device__ __forceinline__ bool nz4(const float4& x) { return x.x != 0.f || x.y != 0.f || x.z != 0.f || x.w != 0.f; }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t w_rsrc(const float* W, unsigned bytes) {
+  const uintptr_t a = (uintptr_t)W;
+  const uintptr_t u = ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 w_load(__amdgpu_buffer_rsrc_t rs, unsigned off, bool use) {
+  using u32x4 = unsigned __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, use ? off : 0xFFFFFFF0u, 0, 0));
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+template <bool SKIP = false>
+__device__ __forceinline__ float row_dot16(const float4* __restrict__ r, const float4* f4, int F4, int sub,
+                                           __amdgpu_buffer_rsrc_t rs, unsigned roff) {
   float a0 = 0.f, a1 = 0.f;
   int q = sub;
   for (; q + 48 < F4; q += 64) {
-    const float4 w0 = r[q], w1 = r[q + 16], w2 = r[q + 32], w3 = r[q + 48];
     const float4 x0 = f4[q], x1 = f4[q + 16], x2 = f4[q + 32], x3 = f4[q + 48];
+    float4 w0, w1, w2, w3;
+    if (SKIP) {
+      w0 = w_load(rs, roff + 16u * q, nz4(x0));
+      w1 = w_load(rs, roff + 16u * (q + 16), nz4(x1));
+      w2 = w_load(rs, roff + 16u * (q + 32), nz4(x2));
+      w3 = w_load(rs, roff + 16u * (q + 48), nz4(x3));
+    } else {
+      w0 = r[q];
+      w1 = r[q + 16];
+      w2 = r[q + 32];
+      w3 = r[q + 48];
+    }
     a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
     a1 += w1.x * x1.x + w1.y * x1.y + w1.z * x1.z + w1.w * x1.w;
     a0 += w2.x * x2.x + w2.y * x2.y + w2.z * x2.z + w2.w * x2.w;
     a1 += w3.x * x3.x + w3.y * x3.y + w3.z * x3.z + w3.w * x3.w;
   }
   for (; q < F4; q += 16) {
-    const float4 w0 = r[q], x0 = f4[q];
+    const float4 x0 = f4[q];
+    const float4 w0 = SKIP ? w_load(rs, roff + 16u * q, nz4(x0)) : r[q];
     a0 += w0.x * x0.x + w0.y * x0.y + w0.z * x0.z + w0.w * x0.w;
   }
   float a = a0 + a1;
@@ -509,7 +543,8 @@ __device__ __forceinline__ float row_dot16(const float4* __restrict__ r, const f
 template <int R = 1>
 __device__ __forceinline__ void leaf_logits_dots(const DevPreset& dp, int lo, int hi, int wave, int nw,
                                                  const float* __restrict__ W, const float* __restrict__ bias, int F,
-                                                 const uint32_t* lds, int32_t* out_ids, float* out_lg) {
+                                                 const uint32_t* lds, int32_t* out_ids, float* out_lg,
+                                                 int skipz = 0) {
   const int32_t* ids = reinterpret_cast<const int32_t*>(lds + dp.W32pad);
   const float* f = reinterpret_cast<const float*>(lds + dp.W32pad + kLeafCap);
   const int l = threadIdx.x & 63;
@@ -558,16 +593,22 @@ __device__ __forceinline__ void leaf_logits_dots(const DevPreset& dp, int lo, in
       }
     }
   } else if ((F & 3) == 0) {
-    // F > 64 kLeafQ: the same sums streamed, every 16th float4 of the row with up to 4 loads in
+    // the streaming path (the default, R = 1): every 16th float4 of the row with up to 4 loads in
     // flight; the 16-lane partial sums meet in 4 xor-shuffles
     const int F4 = F >> 2;
     const float4* f4 = reinterpret_cast<const float4*>(f);
     const int sub = l & 15, quad = l >> 4;
+    // skipz: the W table as a buffer resource (its byte size must fit the 31-bit range)
+    const uint64_t wbytes = (uint64_t)dp.A * (uint64_t)F * 4u;
+    const bool sk = skipz && wbytes < 0x7FFFFFF0ull;
+    const __amdgpu_buffer_rsrc_t wrs = w_rsrc(W, sk ? (unsigned)wbytes : 0u);
     for (int j0 = lo + 4 * wave; j0 < hi; j0 += 4 * nw) {
       const int j = j0 + quad;
       const bool ok = j < hi;
       const int id = ids[ok ? j : lo];
-      const float a = row_dot16(reinterpret_cast<const float4*>(W + (size_t)id * F), f4, F4, sub);
+      const float4* wr = reinterpret_cast<const float4*>(W + (size_t)id * F);
+      const float a = sk ? row_dot16<true>(wr, f4, F4, sub, wrs, (unsigned)id * (unsigned)F * 4u)
+                            : row_dot16<false>(wr, f4, F4, sub, wrs, 0u);
       if (sub == 0 && ok) {
         if (out_ids) out_ids[j] = id;
         out_lg[j] = a + bias[id];
