@@ -159,7 +159,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
                                                                     int32_t* __restrict__ status_out,
                                                                     float* __restrict__ obs,
                                                                     uint64_t* __restrict__ mask_out, int sel_off,
-                                                                    int prio, int skipz) {
+                                                                    int skipz) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ int status_sh, status0_sh;
   __shared__ StepExpand sx;
@@ -219,9 +219,6 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   uint32_t* lsel = lds + sel_off;
   uint32_t* m32 = lsel + kStateWords + 2 * kMaxN;
   if (wave == 0) {
-    // the backup and descent are the step's dependent chain; the logit waves sharing its SIMD
-    // mostly wait on their loads, so wave 0 issues first (prio: A/B knob)
-    if (prio) __builtin_amdgcn_s_setprio(3);
     const StepHead h = backup_first(m, t, dp.P, values, status0);
     if (h.status == 1) {
       // wave 1 adds the new node once the leaf's ids are compacted
@@ -259,7 +256,6 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
       // the step's tail, after the bitmask)
       leaf_obs_rows<1>(dp, m, t, st, obs, lsel, lane_id());
     }
-    if (prio) __builtin_amdgcn_s_setprio(0);
   }
   if (wave > 0 && K >= 0 && K <= kLeafCap) {
     leaf_logits_dots<BK_LEAF_R>(dp, 0, K, wave - 1, kStepWaves - 1, W, bias, F, lds, nullptr, lg, skipz);
@@ -522,13 +518,11 @@ int bk_mcts_leaf_step(bk_mcts* m, const float* feat, int64_t ldf, int F, const f
   if (overlap) {
     const int sel_off = (int)(((size_t)dp.W32pad + 2 * kLeafCap + F + 3) & ~(size_t)3);
     const size_t words = (size_t)sel_off + kStateWords + 2 * kMaxN + dp.W32pad;
-    const char* pr = getenv("BK_STEP_PRIO");  // A/B: wave 0 (backup + descent) at issue priority 3
-    const int prio = pr ? atoi(pr) : 0;
     const char* sz = getenv("BK_LEAF_SKIP0");  // W float4s of all-zero features not loaded (0: load all)
     const int skipz = sz ? atoi(sz) : 1;
     hipLaunchKernelGGL(k_leaf_step_ov, dim3(m->d.T), dim3(kWave * kStepWaves), sizeof(uint32_t) * words,
                        (hipStream_t)stream, dp, m->d, feat, ldf, F, W, bias, values, do_select,
-                       (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, sel_off, prio, skipz);
+                       (const uint32_t*)roots, active, cpuct, leaf_status, obs, leaf_mask, sel_off, skipz);
     return launch_check("k_leaf_step_ov");
   }
   size_t words = (size_t)dp.W32pad + kLeafCap + F;                               // leaf logits
