@@ -120,20 +120,34 @@ def _sum_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def bench_dry(args, world, rank):
-    """--workload dry: the multi-rank launch rehearsed on CPU (gloo, no GPU touched): every rank
-    packs a shard of synthetic replay rows (seeded by rank, ragged counts) and the ranks run the
-    config-4 exchange, all_gather_packed; rank 0 reports which ranks' rows arrived intact."""
+def _dry_rows(rank: int):
+    """Rank r's synthetic replay shard for --workload dry: 3 + r rows (ragged across ranks),
+    K = 40 + 10 r ids each (so the caps differ: 64 for ranks 0-2, 128 above), seeded by rank."""
     from blokus_rl_amd import replay as rp
 
     g = torch.Generator().manual_seed(rank)
     E, K = 3 + rank, 40 + 10 * rank
-    states = torch.full((E, rp.STATE), rank, dtype=torch.uint8)
-    k = torch.full((E,), K, dtype=torch.int32)
-    ids = torch.randint(0, 30433, (E, K), generator=g).to(torch.int16)
-    pi = torch.rand((E, K), generator=g)
-    z = torch.zeros((E, 4))
-    buf, cap = rp.pack(states, ids, pi, k, z)
+    states = torch.randint(0, 256, (E, rp.STATE), dtype=torch.uint8, generator=g)
+    states[:, 0] = rank
+    k = torch.randint(1, K + 1, (E,), generator=g).to(torch.int32)
+    col = torch.arange(K).unsqueeze(0)
+    ids = torch.where(col < k.unsqueeze(1), torch.randint(0, 30433, (E, K), generator=g).to(torch.int16),
+                      torch.full((E, K), -1, dtype=torch.int16))
+    pi = torch.where(col < k.unsqueeze(1), torch.rand((E, K), generator=g), torch.zeros((E, K)))
+    z = torch.tensor([[3.0, -1.0, 1.0, -1.0]]).roll(rank, 1).repeat(E, 1)
+    player = (torch.arange(E, dtype=torch.int32) + rank) % 4
+    return states, ids, pi, k, z, player
+
+
+def bench_dry(args, world, rank):
+    """--workload dry: the multi-rank launch rehearsed on CPU (gloo, no GPU touched): every rank
+    packs a shard of synthetic replay rows (seeded by rank, ragged row counts and caps) and the
+    ranks run the config-4 exchange, all_gather_packed; rank 0 checks every rank's rows against
+    their generator, field by field (`rows_intact`), and reports which ranks' rows arrived."""
+    from blokus_rl_amd import replay as rp
+
+    states, ids, pi, k, z, player = _dry_rows(rank)
+    buf, cap = rp.pack(states, ids, pi, k, z, player)
     _barrier(world)
     t0 = time.perf_counter()
     if dist_active():
@@ -144,10 +158,22 @@ def bench_dry(args, world, rank):
     dt = _max_over_ranks(time.perf_counter() - t0, world)
     u = rp.unpack(rows, cap)
     seen = sorted({int(s) for s in u["states"][:, 0].tolist()})
+    intact, off = True, 0
+    for r in range(world):
+        st_r, ids_r, pi_r, k_r, z_r, pl_r = _dry_rows(r)
+        E, K = ids_r.shape
+        sl = slice(off, off + E)
+        intact &= (torch.equal(u["states"][sl], st_r) and torch.equal(u["k"][sl], k_r)
+                   and torch.equal(u["player"][sl], pl_r) and torch.equal(u["z"][sl], z_r)
+                   and torch.equal(u["ids"][sl, :K], ids_r) and torch.equal(u["pi"][sl, :K], pi_r)
+                   and bool((u["ids"][sl, K:] == -1).all()) and bool((u["pi"][sl, K:] == 0).all()))
+        off += E
+    intact &= off == rows.shape[0]
     return {"metric": "launch rehearsal (gloo, CPU): replay rows all-gathered", "value": float(rows.shape[0]),
             "unit": "rows", "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": dt * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": "dry", "parallelism": f"dp{world}"}, "ranks_seen": seen,
+            "rows_intact": bool(intact), "common_cap": cap,
             "backend": dist.get_backend() if dist_active() else None}
 
 

@@ -78,6 +78,14 @@ class LeafEvaluator:
             po = self.model.f.policy_out
             self.policy_w = po.weight.detach().float().contiguous()
             self.policy_b = po.bias.detach().float().contiguous()
+            # the sparse head leaves out W float4s whose four features are zero (exact: 0 * w adds
+            # +-0 for finite w); a non-finite weight there would have made the reference's logit
+            # NaN, so a diverged policy layer is refused here instead of silently giving finite priors
+            if not (bool(torch.isfinite(self.policy_w).all()) and bool(torch.isfinite(self.policy_b).all())):
+                from ..engine import EngineError
+
+                raise EngineError("the policy layer holds non-finite weights (diverged net): refusing the sparse "
+                                  "policy head, whose zero-feature skip would hide the NaN logits")
         # the HIP ResNet reads the planar observation k_select writes (the search can write straight
         # into static_obs: no copy); the MIOpen paths want channels_last
         self.planar = isinstance(self.model, LeafResNet) and self.model.native
@@ -177,6 +185,7 @@ class SelfPlay:
         # an active game whose root had more children than `cap` (k_root returns counts = -K):
         # latched on the device, raised by check() at the next host sync
         self._cap_overflow = torch.zeros((), dtype=torch.int32, device=dev)
+        self.last_action = torch.full((games,), -1, dtype=torch.int32, device=dev)
 
     @staticmethod
     def max_game_plies(eng: Engine) -> int:
@@ -362,6 +371,7 @@ class SelfPlay:
                 self._dropped_plies += len(self._records) - self.record_plies
                 del self._records[:-self.record_plies]
                 del self._window[:-self.record_plies]
+        self.last_action = action
         self.roots, _, status = self.eng.next_state(self.roots, action)
         self.first_ply &= ~act_mask
         self._stats.plies += 1
@@ -400,6 +410,7 @@ class SelfPlay:
                 self._dropped_plies += len(self._records) - self.record_plies
                 del self._records[:-self.record_plies]
                 del self._window[:-self.record_plies]
+        self.last_action = action  # the ply's sampled action per game (-1: none), for checkers
         nxt, _, status = eng.next_state(self.roots, action)
         ended, scores = eng.game_ended(nxt)
         self._stats.plies += 1
@@ -441,7 +452,8 @@ class SelfPlay:
 
     def window_packed(self):
         """Packed replay rows (blokus_rl_amd.replay layout) of every ply recorded since
-        mark_window(); z is zero for games still running (their outcome is not known yet)."""
+        mark_window(). z is the final one-hot score of the row's game (trainer.py:131-135) for
+        games that have ended, zero for games still running (their outcome is not known yet)."""
         from ..replay import pack
 
         if not self._window:
@@ -454,7 +466,8 @@ class SelfPlay:
         ids = torch.cat([r[1][:, :cap] for r in self._window])[m]
         pi = torch.cat([r[2][:, :cap] for r in self._window])[m]
         player = torch.cat([r[4] for r in self._window])[m]
-        z = torch.zeros((states.shape[0], self.eng.P), dtype=torch.float32, device=self.eng.device)
+        gids = torch.cat([r[5] for r in self._window])[m]
+        z = torch.where(self.z_known[gids].unsqueeze(1), self.z_table[gids], torch.zeros_like(self.z_table[gids]))
         return pack(states, ids, pi, k, z, player, cap=cap)
 
     def run(self, plies: int, check_every: int = 8):

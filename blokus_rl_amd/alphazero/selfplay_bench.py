@@ -291,7 +291,6 @@ def bench_selfplay(args, world, rank):
                   "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
                   "traffic": None, "bytes_per_sim_step": sbytes / steps_sim, "search_ms_per_sim_step": search_ms}
     late = late_game(sp, getattr(args, "late_plies", 0), args.warmup + args.steps + 1)
-    ks = ms.pop("k_sims", None)
     out = {
         "metric": "MCTS sims/sec on 20x20 Blokus (4 players, 256 games/GPU, 100 sims/move)",
         "value": sims / elapsed,
@@ -326,17 +325,4 @@ def bench_selfplay(args, world, rank):
         out["roofline"] = out["tower_roofline"]
     else:
         out["roofline"] = out["search_roofline"]
-    if ks is not None:
-        # the fused path: a ply's simulations are k_sims launches, the only kernel of the sim-steps;
-        # its FLOP = the MFMA work of the leaf nets (stem + Winograd tower) of the leaves it expanded
-        tf = ks["flop"] / (ks["ms"] * 1e-3)
-        out["roofline"] = {
-            "bound": "mfma",
-            "kernel": "k_sims (a ply's %d simulations in %d launch(es), one workgroup per tree: select, the leaf "
-                      "ResNet - stem + %d Winograd F(2x2,3x3) f32 MFMA convs + heads - the sparse policy head, "
-                      "expand/backup)" % (ks["sims"], ks["launches"], ks["convs"]),
-            "achieved": tf / 1e12, "peak": FP32_PEAK / 1e12, "unit": "TFLOP/s", "frac": tf / FP32_PEAK,
-            "traffic": None, "kernel_ms": ks["ms"] / ks["launches"], "flop_per_launch": ks["flop"] / ks["launches"],
-            "units_per_launch": ks["leaves"] / ks["launches"], "flop_per_leaf": ks["flop_per_leaf"],
-            "launches_per_ply": ks["launches"], "share_of_ply": ks["ms"] / (elapsed / args.steps * 1e3)}
     return out

@@ -110,11 +110,10 @@ __device__ __forceinline__ float wave_max_f(float x) {
 }
 
 // LDS handoff between the lanes of the one wave that owns a board, in the board-level helpers
-// below and the search's per-tree stages (mcts_dev.h). Their per-stage kernels are 64-thread
-// workgroups and keep the barrier; sims.hip runs those stages on one wave of a 4-wave workgroup
-// (the other waves wait elsewhere meanwhile) and defines BK_BOARD_SYNC() as wave_lds_sync(): a
-// wave's LDS operations complete in issue order, so only the compiler must be kept from moving
-// LDS accesses across the handoff.
+// below and the search's per-tree stages (mcts_dev.h). Their kernels are 64-thread workgroups
+// and keep the barrier; a kernel that runs those stages on one wave of a larger workgroup can
+// define BK_BOARD_SYNC() as wave_lds_sync() instead: a wave's LDS operations complete in issue
+// order, so only the compiler must be kept from moving LDS accesses across the handoff.
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -1,6 +1,6 @@
 // leafnet_common.h — pieces shared by the leaf-net kernels on split-f16 MFMA products
-// (leafnet.hip: direct convolutions; leafnet_wino.hip: Winograd F(2x2,3x3) tower): the operand
-// split, power-of-two scaling, the stem's pixel map and direct K-chunk loop, the MFMA drain.
+// (leafnet.hip: k_leafnet_x3, direct convolutions): the operand split, power-of-two scaling, the
+// stem's pixel map and direct K-chunk loop, the MFMA drain.
 #pragma once
 #include "../../include/blokus_engine.h"
 #include "ctx.h"

@@ -1,7 +1,7 @@
 // mcts_dev.h — device state of the batched search and its per-tree stages (select_tree,
 // leaf_logits_tree, expand_tree), shared by the per-stage kernels (mcts.hip: one launch per stage
-// over all trees) and the fused simulation kernels (sims.hip: one workgroup runs whole simulations
-// of one tree). Design notes and the reference mapping: mcts.hip.
+// over all trees) and the fused leaf step (k_leaf_step / k_leaf_step_ov, mcts.hip). Design notes
+// and the reference mapping: mcts.hip.
 #pragma once
 #include <cmath>
 #include <vector>
@@ -425,7 +425,7 @@ __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& 
   BK_STAMP(0, 5);
 }
 
-// k_select's work on tree t by one wave (k_sims, k_sims_const): descent + leaf.
+// k_select's work on tree t by one wave: descent + leaf.
 __device__ __forceinline__ int select_tree(const DevPreset& dp, const DevMcts& m, int t,
                                            const uint32_t* __restrict__ roots, const int32_t* __restrict__ active,
                                            double cpuct, int32_t* __restrict__ status_out, float* __restrict__ obs,
@@ -631,7 +631,7 @@ __device__ __forceinline__ void leaf_logits_dots(const DevPreset& dp, int lo, in
 
 
 // k_leaf_logits' work on tree t by a workgroup of any multiple of 64 threads, share c of nc, R x 4
-// ids per wave at a time (k_sims: the whole tree, nc 1, R 2): lds = W32pad + kLeafCap + F words.
+// ids per wave at a time: lds = W32pad + kLeafCap + F words.
 template <int R = 1>
 __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevMcts& m, int t, int c, int nc,
                                                  const float* __restrict__ feat, int64_t ldf, int F,
@@ -650,7 +650,7 @@ __device__ __forceinline__ void leaf_logits_tree(const DevPreset& dp, const DevM
 //               the same softmax, no compaction or gather here;
 // prior_mode 1: logp holds the prior itself at the legal ids (test hook: identical P fed to the
 //               reference and to this engine).
-// k_expand_backup's work on tree t, by one wave (k_sims runs it too): lds = W32pad + kExpandLdsIds words
+// k_expand_backup's work on tree t, by one wave: lds = W32pad + kExpandLdsIds words
 // The tree's scalars, the table probe, the logits and the path records are loaded in as few
 // dependent round trips as the data allows: (1) status, depth, node/child counters, leaf key and
 // K together; (2) the probe, the logit gather and the path records together; (3) the path

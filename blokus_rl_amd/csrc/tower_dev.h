@@ -1,6 +1,6 @@
 // tower_dev.h — device code of the Winograd form-2 convolution (k_conv3x3_wino2) and of the leaf
-// net in one workgroup per board (tower_forward: stem, residual tower, heads), shared by conv.hip
-// (k_conv3x3_wino2, k_tower_wino) and sims.hip (k_sims). Design notes: conv.hip.
+// net in one workgroup per board (tower_forward: stem, residual tower, heads), used by conv.hip
+// (k_conv3x3_wino2, k_tower_wino). Design notes: conv.hip.
 #pragma once
 #include "ctx.h"
 
@@ -531,8 +531,7 @@ struct TowerHeads {
   const float* bstem;
 };
 
-// The leaf net of board blockIdx.x: k_tower_wino's body (k_sims runs it inside its simulation
-// loop). v_lds: [2 buf][16 s][16 p][16 t][4 g] (+ the heads' partials [NN][4][3] with HEADS).
+// The leaf net of board blockIdx.x: k_tower_wino's body. v_lds: [2 buf][16 s][16 p][16 t][4 g] (+ the heads' partials [NN][4][3] with HEADS).
 template <int N, bool HEADS, bool STEM = false>
 __device__ __forceinline__ void tower_forward(float* v_lds, const float* __restrict__ x0, float* hA, float* hB,
                                               float* __restrict__ out, const float* __restrict__ u2all,

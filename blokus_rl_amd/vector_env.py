@@ -54,8 +54,12 @@ class BlokusVectorEnv:
 
     def step_raw(self, actions: torch.Tensor | None = None):
         """The env step alone (one bk_vec_step launch, no result tensors built): obs, mask_words,
-        reward and done are updated in place. Capturable in a HIP graph."""
-        act = None if actions is None else actions
+        reward and done are updated in place. Capturable in a HIP graph (the checks are host-side)."""
+        act = actions
+        if act is not None:
+            if not (act.is_cuda and act.device == torch.device(self.device) and act.dtype == torch.int32
+                    and act.is_contiguous() and act.numel() == self.num_envs):
+                raise ValueError("step_raw wants a contiguous int32 [num_envs] tensor on the env's device")
         _check(self.eng.lib.bk_vec_step(self.eng.h, _ptr(self.states), _ptr(self.rng), _ptr(act), self.num_envs,
                                         _ptr(self.obs), _ptr(self.mask_words), _ptr(self.reward), _ptr(self.done),
                                         self._s()))

@@ -86,3 +86,24 @@ def test_bench_launches_ranks_itself():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["ranks_seen"] == [0, 1] and out["value"] == 3 + 4
+    assert out["rows_intact"]
+
+
+def test_bench_dry_world8_rows_intact():
+    """The config-4 rank count: `bench.py --gpus 8 --workload dry` launches 8
+    gloo ranks on CPU; every rank's ragged shard (3 + r rows, caps 64 and 128) must reach rank 0
+    through all_gather_packed bit for bit, in rank order."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--workload", "dry"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["ranks_seen"] == list(range(8))
+    assert out["rows_intact"] and out["value"] == sum(3 + r for r in range(8)) and out["common_cap"] == 128

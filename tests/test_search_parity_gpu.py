@@ -24,11 +24,17 @@ T, SIMS, BLOCKS = 64, 100, 5
 def _dump_trees(sp, eng, o, roots_h, more=()):
     """BFS over every tree through visited children from its root (and the roots in `more`):
     {tree: {hash: (state, ids, N, Q, P)}}."""
+    return _dump_forest(sp, eng, o, [[roots_h[t]] + [r[t] for r in more] for t in range(T)])
+
+
+def _dump_forest(sp, eng, o, starts):
+    """BFS over every tree t through visited children from each state of starts[t]."""
     trees = [dict() for _ in range(T)]
-    frontier = [[roots_h[t]] + [r[t] for r in more] for t in range(T)]
+    frontier = [list(s) for s in starts]
+    state_bytes = starts[0][0].shape[0]
     cap = 2048
     while any(frontier):
-        q = np.zeros((T, roots_h.shape[1]), dtype=np.uint8)
+        q = np.zeros((T, state_bytes), dtype=np.uint8)
         act = np.zeros(T, dtype=np.int32)
         cur = [None] * T
         for t in range(T):
@@ -196,3 +202,141 @@ def test_config3_tree_reuse_matches_oracle_replay():
             rids, rpi, rk = pis[i]
             K = int(rk[t])
             assert (rids[t, :K] == oids).all() and rpi[t, :K].tolist() == d.tolist(), (t, i)
+
+
+TURN_PLIES = 5
+
+
+def _near_terminal_roots(o):
+    """Root t: a uniform-random game of the oracle (default_rng(1000 + t)) played to its end (52-64
+    plies), backed up by 1 + t % 8 plies, so about half of the games end inside TURN_PLIES."""
+    roots = []
+    for t in range(T):
+        rng = np.random.default_rng(1000 + t)
+        hist = [o.init_state()]
+        while o.game_ended(hist[-1]) is None:
+            ids = o.legal_ids(hist[-1])
+            hist.append(o.next_state(hist[-1], int(ids[int(rng.integers(len(ids)))]))[0])
+        roots.append(hist[-1 - (1 + t % 8)])
+    return np.stack(roots)
+
+
+def test_config3_game_turnover_matches_oracle_replay():
+    """Game turnover on the production path: SelfPlay(continuous=True).play_ply
+    on 64 trees at config-3 shape (20x20, 5-block net, 100 sims) from near-terminal roots, so
+    games end, their trees are reset (k_reset: a new MCTS per episode, trainer.py:95) and their
+    slots restart from the empty board (k_ply_finish) inside the window. Each slot is replayed
+    through one MCTSOracle per episode — persistent while the game runs, a fresh one for the
+    restarted game — with the GPU's leaf evaluations: every node's N and float64 Q and each ply's
+    root pi bit-exact at every ply, the restarted games' first plies included. The next roots are
+    the oracle's next states (or the empty board after a game end), and z of every finished game,
+    in the z table and in the rows of window_packed(), is the oracle's final one-hot score of that
+    game (trainer.py:131-135); rows of running games carry z = 0."""
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine
+    from blokus_rl_amd.nets import ResNet, net_math
+    from blokus_rl_amd.replay import unpack
+
+    eng = Engine(20, 4, 5)
+    o = Oracle(20, 4, 5)
+    torch.manual_seed(0)
+    model = ResNet(20, 4, eng.A, num_res_blocks=BLOCKS).to(eng.device).eval()
+    sp = SelfPlay(eng, model, T, num_sims=SIMS, seed=5, continuous=True)
+    assert sp._graph_usable() and net_math() == "x3"
+    init = o.init_state()
+    sp.roots = torch.from_numpy(_near_terminal_roots(o)).to(eng.device)
+    sp.mark_window()
+    episode_roots = [[r] for r in sp.roots.cpu().numpy()]  # roots of each slot's running episode
+    plies = []  # per ply: roots, game ids, dumps, root pi, actions, ended scores per slot
+    for i in range(TURN_PLIES):
+        roots_h = sp.roots.cpu().numpy()
+        gid = sp.game_id.cpu().numpy().copy()
+        for t in range(T):
+            if i > 0 and not (roots_h[t] == episode_roots[t][-1]).all():
+                episode_roots[t].append(roots_h[t])
+        sp._simulations(sp.num_sims)  # = play_ply: the simulations, then the fused ply tail
+        dump = _dump_forest(sp, eng, o, episode_roots)
+        pol = tuple(x.cpu().numpy() for x in sp.mcts.root_policy(sp.roots, None, 1.0))
+        sp._ply_tail_fused(True)
+        sp.check()
+        act = sp.last_action.cpu().numpy()
+        nxt_h = sp.roots.cpu().numpy()
+        ends = [None] * T
+        for t in range(T):
+            assert act[t] >= 0, (i, t)
+            s2, _ = o.next_state(roots_h[t], int(act[t]))
+            ends[t] = o.game_ended(s2)
+            if ends[t] is None:
+                assert (nxt_h[t] == s2).all(), (i, t)
+            else:
+                # the finished game's z, and its slot restarted from the empty board with a new tree
+                assert (nxt_h[t] == init).all(), (i, t)
+                assert sp.z_table[int(gid[t])].cpu().numpy().tolist() == ends[t].tolist(), (i, t)
+                episode_roots[t] = [init]
+        plies.append((roots_h, gid, dump, pol, ends))
+    ended = sum(e is not None for p in plies for e in p[4])
+    restarted = [t for t in range(T) if any(p[4][t] is not None for p in plies[:-1])]
+    assert ended >= 16 and len(restarted) >= 8, (ended, len(restarted))
+
+    # leaf values of every node, recomputed by the same net (a value depends on the state only)
+    vals, states = {}, {}
+    for p in plies:
+        for tr in p[2]:
+            for h, nd in tr.items():
+                states.setdefault(h, nd[0])
+    hs = list(states)
+    ev = sp.evaluator
+    for j in range(0, len(hs), T):
+        chunk = hs[j:j + T]
+        st = np.zeros((T, init.shape[0]), dtype=np.uint8)
+        for r, h in enumerate(chunk):
+            st[r] = states[h]
+        _, v = ev._forward(eng.observe(torch.from_numpy(st).to(eng.device)))
+        v = v.cpu().numpy()
+        for r, h in enumerate(chunk):
+            vals[h] = v[r].astype(np.float64)
+
+    for t in range(T):
+        cur = {}
+
+        def evaluate(s, player):
+            h = o.hash(s)
+            _, ids, _, _, P = cur["nodes"][h]
+            assert (ids == o.legal_ids(s, player)).all()
+            return ids, P, vals[h]
+
+        m = None
+        for i, (roots_h, _, dump, pol, ends) in enumerate(plies):
+            nodes = cur["nodes"] = dump[t]
+            if m is None:
+                m = MCTSOracle(o, evaluate)
+            for _ in range(SIMS):
+                m.simulate(roots_h[t], cpuct=sp.cpuct)
+            assert set(m.tree) == set(nodes), (t, i)
+            for h, nd in m.tree.items():
+                _, _, N, Q, _ = nodes[h]
+                assert nd["N"] == N.tolist(), (t, i, h)
+                assert nd["Q"] == Q.tolist(), (t, i, h)
+            oids, d = m.get_distribution(roots_h[t], 1.0)
+            rids, rpi, rk = pol
+            K = int(rk[t])
+            assert (rids[t, :K] == oids).all() and rpi[t, :K].tolist() == d.tolist(), (t, i)
+            if ends[t] is not None:
+                m = None  # the episode is over: the next ply's search starts a fresh tree (trainer.py:95)
+
+    # the window's rows: ply-major, one per slot; z = the final score of the row's game once it ended
+    buf, cap = sp.window_packed()
+    rows = unpack(buf, cap)
+    assert rows["states"].shape[0] == TURN_PLIES * T
+    zrow = rows["z"].cpu().numpy()
+    final = {}
+    for p in plies:
+        for t in range(T):
+            if p[4][t] is not None:
+                final[int(p[1][t])] = p[4][t]
+    for i, p in enumerate(plies):
+        for t in range(T):
+            r = i * T + t
+            assert (rows["states"][r].cpu().numpy() == p[0][t]).all()
+            want = final.get(int(p[1][t]), np.zeros(4))
+            assert zrow[r].tolist() == want.tolist(), (i, t)

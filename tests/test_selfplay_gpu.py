@@ -121,6 +121,22 @@ def test_selfplay_raises_when_root_exceeds_cap():
         sp.run(2)
 
 
+def test_selfplay_refuses_non_finite_policy_weights():
+    """the sparse policy head skips W float4s of zero features, exact only for finite
+    weights; a diverged policy layer (a NaN weight) is refused when the evaluator caches it."""
+    from blokus_rl_amd.alphazero.selfplay import SelfPlay
+    from blokus_rl_amd.engine import Engine, EngineError
+    from blokus_rl_amd.nets import ResNet
+
+    eng = Engine(7, 2, 5)
+    torch.manual_seed(0)
+    net = ResNet(7, 2, eng.A, 1).to(eng.device).eval()
+    with torch.no_grad():
+        net.policy_out.weight[5, 3] = float("nan")
+    with pytest.raises(EngineError):
+        SelfPlay(eng, net, 4, num_sims=2, seed=0)
+
+
 def test_play_ply_sampling_statistics():
     """SelfPlay.play_ply's sampling against the reference episode's law (trainer.py:108-135):
     on the first ply pi = 0.75 pi_search + 0.25 Dir(1) (one noise draw per game), the action is a

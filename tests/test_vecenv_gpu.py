@@ -1,6 +1,10 @@
 """Config-5 vector env on the GPU against its CPU restatement (oracle/vecenv_oracle.py):
-states, observations, masks, rewards and dones bit-exact over many steps and episodes, with
-agent actions both given (random legal, chosen on the host) and drawn in-kernel."""
+states, observations, masks, rewards, dones and the per-env random streams bit-exact over many
+steps and episodes — agent actions given (random legal ids chosen on the host, plus out-of-range
+and illegal ids, which end the episode as a loss) and drawn in-kernel; a partial last workgroup
+(E not a multiple of the envs per workgroup), both lane widths of k_vec_step7 and the
+one-wave-per-env kernel; and the benchmark size (8192 envs, and 8190) driven through a captured
+HIP graph of back-to-back step_raw launches as bench.py replays it (ppo/trainer.py:128-175)."""
 import numpy as np
 import pytest
 import torch
@@ -10,37 +14,127 @@ from oracle.vecenv_oracle import VecEnvOracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("max_cells", [4, 5])
-def test_vector_env_matches_oracle(max_cells):
+def _obs_of(states: np.ndarray, N: int = 7) -> np.ndarray:
+    """VecEnvOracle.obs for every env at once: 1 where colour 0 sits, 2 for colour 1, else 0."""
+    occ = np.ascontiguousarray(states[:, :320]).view(np.uint32).reshape(-1, 4, 20)[:, :2, :N]
+    bits = (occ[..., None] >> np.arange(N, dtype=np.uint32)) & 1
+    return np.where(bits[:, 0] == 1, 1, np.where(bits[:, 1] == 1, 2, 0)).astype(np.uint8)
+
+
+def _assert_env_equal(env, ref, tag):
+    E = env.num_envs
+    st = env.states.cpu().numpy()
+    want = np.stack(ref.states)
+    bad = np.nonzero((st != want).any(axis=1))[0]
+    assert bad.size == 0, (tag, "state", bad[:8])
+    assert (env.obs.cpu().numpy() == _obs_of(want)).all(), (tag, "obs")
+    m = env.mask_words.cpu().numpy().view(np.uint64)
+    for e in range(E):
+        assert (m[e] == ref.mask(e)).all(), (tag, "mask", e)
+    assert (env.rng.cpu().numpy().view(np.uint64) == np.array(ref.rng, dtype=np.uint64)).all(), (tag, "rng")
+
+
+@pytest.mark.parametrize("max_cells,E,kernel", [(4, 32, "16"), (5, 32, "16"), (4, 37, "16"), (5, 37, "8"),
+                                                (4, 32, "8"), (4, 37, "wave")])
+def test_vector_env_matches_oracle(max_cells, E, kernel, monkeypatch):
+    """E = 37: the last workgroup holds 5 (16 lanes) or 5 of 32 (8 lanes) envs — spare lane groups
+    and the byte-wise obs copy. kernel: lanes per env of k_vec_step7 (BK_VEC_LANES), or the
+    one-wave-per-env k_vec_step (BK_VEC_WAVE=1). Every 7th step gives each env an out-of-range id
+    (>= A) or an id that is in range but not legal: reward -1, done, auto-reset, rng untouched."""
     from blokus_rl_amd.vector_env import BlokusVectorEnv
 
-    E = 32
+    if kernel == "wave":
+        monkeypatch.setenv("BK_VEC_WAVE", "1")
+    else:
+        monkeypatch.setenv("BK_VEC_LANES", kernel)
     env = BlokusVectorEnv(E, 7, max_cells)
     ref = VecEnvOracle(E, 7, max_cells)
+    A = env.eng.A
     env.reset(seed=5)
     ref.reset(seed=5)
     rng = np.random.default_rng(0)
-    episodes = 0
+    episodes = losses = 0
     for t in range(60):
+        _assert_env_equal(env, ref, t)
         m = env.mask_words.cpu().numpy().view(np.uint64)
-        obs = env.obs.cpu().numpy()
-        for e in range(E):
-            assert (m[e] == ref.mask(e)).all(), (t, e)
-            assert (obs[e] == ref.obs(e)).all(), (t, e)
-            assert (env.states[e].cpu().numpy() == ref.states[e]).all(), (t, e)
-        if t % 3 == 2:
+        legal = [np.nonzero(np.unpackbits(m[e].view(np.uint8), bitorder="little")[:A])[0] for e in range(E)]
+        if t % 7 == 6:
+            acts = np.empty(E, dtype=np.int32)
+            for e in range(E):
+                if e % 3 == 0:
+                    acts[e] = A + int(rng.integers(0, 4096))  # out of range
+                else:
+                    illegal = np.setdiff1d(np.arange(A), legal[e])
+                    acts[e] = int(rng.choice(illegal)) if e % 3 == 1 else int(rng.choice(legal[e]))
+        elif t % 3 == 2:
             acts = np.full(E, -1, dtype=np.int32)  # in-kernel random agent
         else:
-            acts = np.array([int(rng.choice(np.nonzero(np.unpackbits(m[e].view(np.uint8), bitorder="little")[:env.eng.A])[0]))
-                             for e in range(E)], dtype=np.int32)
+            acts = np.array([int(rng.choice(legal[e])) for e in range(E)], dtype=np.int32)
         _, rew, term, _, _ = env.step(torch.from_numpy(acts))
         rew, term = rew.cpu().numpy(), term.cpu().numpy()
         for e in range(E):
             r, d = ref.step(e, int(acts[e]))
             assert rew[e] == r and bool(term[e]) == bool(d), (t, e)
             episodes += d
-        assert (env.rng.cpu().numpy().view(np.uint64) == np.array(ref.rng, dtype=np.uint64)).all()
-    assert episodes > E  # several episodes per env ended and auto-reset
+            if t % 7 == 6 and e % 3 != 2:
+                assert r == -1.0 and d == 1, (t, e)
+                losses += 1
+    _assert_env_equal(env, ref, "end")
+    assert episodes > E and losses > 0  # several episodes per env ended and auto-reset
+
+
+def _graph_rollout(E, steps_per_graph, replays, seed):
+    """The bench's config-5 loop: a HIP graph of `steps_per_graph` in-kernel-agent step_raw
+    launches, replayed; the env checked against the oracle after every replay."""
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    env = BlokusVectorEnv(E, 7, 4)
+    ref = VecEnvOracle(E, 7, 4)
+    env.reset(seed=seed)
+    ref.reset(seed=seed)
+    g = torch.cuda.CUDAGraph()
+    # capture on a side stream, as torch.cuda.graph does; nothing runs until the first replay
+    with torch.cuda.graph(g):
+        for _ in range(steps_per_graph):
+            env.step_raw(None)
+    torch.cuda.synchronize()
+    _assert_env_equal(env, ref, "reset")
+    ended = 0
+    for r in range(replays):
+        g.replay()
+        torch.cuda.synchronize()
+        for _ in range(steps_per_graph):
+            last = [ref.step(e, -1) for e in range(E)]
+            ended += sum(d for _, d in last)
+        _assert_env_equal(env, ref, r)
+        rew, done = env.reward.cpu().numpy(), env.done.cpu().numpy()
+        assert rew.tolist() == [x for x, _ in last] and done.tolist() == [d for _, d in last], r
+    return ended
+
+
+def test_vector_env_benchmark_size_graph_matches_oracle():
+    """8192 envs (config 5), the bench's 25-step graph replayed once: 25 back-to-back launches,
+    thousands of episodes ending and auto-resetting inside the graph."""
+    assert _graph_rollout(8192, 25, 1, seed=3) > 8192
+
+
+def test_vector_env_ragged_size_graph_matches_oracle():
+    """8190 envs: not a multiple of the 16 envs of a k_vec_step7 workgroup (the last one holds
+    14); a 5-step graph replayed 4 times, checked after each replay."""
+    assert _graph_rollout(8190, 5, 4, seed=9) > 8190
+
+
+def test_step_raw_rejects_bad_action_tensors():
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    env = BlokusVectorEnv(8, 7, 4)
+    env.reset(seed=0)
+    for bad in (torch.zeros(8, dtype=torch.int32), torch.zeros(8, dtype=torch.int64, device=env.device),
+                torch.zeros(7, dtype=torch.int32, device=env.device),
+                torch.zeros(16, dtype=torch.int32, device=env.device)[::2]):
+        with pytest.raises(ValueError):
+            env.step_raw(bad)
+    env.step_raw(torch.full((8,), -1, dtype=torch.int32, device=env.device))
 
 
 def test_ai_possible_indexes_and_masked_logits():
