@@ -83,6 +83,9 @@ _SIGS = {
     "bk_leafnet_x3_weight_bytes": (_i, [_i]),
     "bk_leafnet_x3_supported": (_i, [_i]),
     "bk_leafnet_x3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8 + [_i, _vp, _vp, _vp, _vp]),
+    "bk_leafnet_w3_weight_bytes": (_i, []),
+    "bk_leafnet_w3_supported": (_i, [_i]),
+    "bk_leafnet_w3": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp] + [_vp] * 8 + [_i, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _LIB = None

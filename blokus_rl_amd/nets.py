@@ -298,15 +298,38 @@ def pack_x3(w: torch.Tensor, b: torch.Tensor | None = None) -> tuple[torch.Tenso
     return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous(), bound.to(w.device)
 
 
+def pack_w3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """[64, 64, 3, 3] tower conv weights -> bk_leafnet_w3's operands: the Winograd F(2x2,3x3)
+    transform U = G w G^T (fp64), each output channel's row scaled by 2^e_o so that its largest
+    |U| lies in [2^14, 2^15), split hi = f16(x), lo = f16(x - hi); and the inverse scales 2^-e_o
+    (f32 [64]). Fragment order [pos 16][chunk 2][wave 4][part hi/lo][lane 64][8 f16]: lane
+    l = 16 g + r of wave w holds U[16 w + r][32 chunk + 8 g + i][pos], i = 0..7 (the A operand of
+    v_mfma_f32_16x16x32_f16 for output channels 16 w.., input channels 32 chunk..)."""
+    assert w.shape == (64, 64, 3, 3)
+    G = torch.tensor(_WINO_G, dtype=torch.float64)
+    U = torch.einsum("ik,ockl,jl->ocij", G, w.detach().to("cpu", torch.float64), G).reshape(64, 64, 16)
+    mx = U.abs().amax(dim=(1, 2))
+    _, e = torch.frexp(mx)
+    e = torch.where(mx > 0, 15 - e, torch.zeros_like(e)).to(torch.float64)
+    scaled = U * torch.pow(2.0, e).view(64, 1, 1)
+    hi = scaled.to(torch.float16)
+    lo = (scaled - hi.to(torch.float64)).to(torch.float16)
+    parts = torch.stack([hi, lo]).view(2, 4, 16, 2, 4, 8, 16)      # [part][wave][row][chunk][g][i][pos]
+    packed = parts.permute(6, 3, 1, 0, 4, 2, 5).contiguous()       # [pos][chunk][wave][part][g][row][i]
+    inv = torch.pow(2.0, -e).to(torch.float32)
+    return packed.view(torch.uint8).view(-1).to(w.device), inv.to(w.device).contiguous()
+
+
 def net_math() -> str:
     """The leaf ResNet's arithmetic on the device: "x3" (default) = bk_leafnet_x3, split-f16 MFMA
-    products with f32 accumulation (fp32-class accuracy, tests/test_leafnet_gpu.py); "f32" =
-    the round-1 kernels on the f32 MFMA (BK_NET_MATH=f32)."""
+    products with f32 accumulation (fp32-class accuracy, tests/test_leafnet_gpu.py); "w3" =
+    bk_leafnet_w3, the same products with the residual tower as Winograd F(2x2,3x3) convolutions
+    (2.25x fewer products per output); "f32" = the round-1 kernels on the f32 MFMA (BK_NET_MATH)."""
     import os
 
     m = os.environ.get("BK_NET_MATH", "x3")
-    if m not in ("x3", "f32"):
-        raise ValueError(f"BK_NET_MATH must be x3 or f32, got {m!r}")
+    if m not in ("x3", "w3", "f32"):
+        raise ValueError(f"BK_NET_MATH must be x3, w3 or f32, got {m!r}")
     return m
 
 
@@ -333,6 +356,39 @@ def leafnet_x3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
         _ptr(model.x3_wtower), _ptr(model.x3_stower), _ptr(model.b_tower), _ptr(model.x3_bounds),
         *[_ptr(t) for t in h[1:]], P, _ptr(pf),
         _ptr(v), None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
+    return (pf, v, out) if want_out else (pf, v)
+
+
+_W3_WS: dict = {}
+
+
+def leafnet_w3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
+    """bk_leafnet_w3: leafnet_x3's network and outputs with the residual tower as Winograd
+    F(2x2,3x3) convolutions on split-f16 products (20x20 boards)."""
+    from .engine import _check, _ptr, _stream, load_library
+
+    B, cin, N, _ = obs.shape
+    assert cin == 8 and obs.dtype == torch.float32 and obs.is_contiguous()
+    f = model.f
+    lib = load_library()
+    nl = 2 * len(f.blocks)
+    assert model.w3_utower.numel() == nl * lib.bk_leafnet_w3_weight_bytes()
+    P = f.value_fc2.out_features
+    pf = torch.empty((B, 2 * N * N), dtype=torch.float32, device=obs.device)
+    v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
+    out = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device,
+                      memory_format=torch.channels_last) if want_out else None
+    # the stem output's workspace, kept per device and batch (a captured graph reuses the pointer)
+    key = (obs.device, B, N)
+    ws = _W3_WS.get(key)
+    if ws is None:
+        ws = _W3_WS[key] = torch.empty((B, N * N, 64), dtype=torch.float32, device=obs.device)
+    h = model.x3_heads
+    _check(lib.bk_leafnet_w3(
+        ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,
+        _ptr(model.w3_utower), _ptr(model.w3_stower), _ptr(model.b_tower), _ptr(model.x3_bounds),
+        *[_ptr(t) for t in h[1:]], P, _ptr(pf), _ptr(v), _ptr(ws),
+        None if out is None else ctypes.c_void_p(out.data_ptr()), _stream(obs.device)))
     return (pf, v, out) if want_out else (pf, v)
 
 
@@ -472,6 +528,10 @@ class LeafResNet(nn.Module):
                 self.register_buffer("x3_wtower", torch.cat([p[0] for p in packs]).contiguous())
                 self.register_buffer("x3_stower", torch.cat([p[1] for p in packs]).contiguous())
                 self.register_buffer("x3_bounds", torch.cat([bs] + [p[2] for p in packs]).contiguous())
+                # bk_leafnet_w3's tower operands: split Winograd U + inverse scales
+                w3 = [pack_w3(c.weight) for c in convs]
+                self.register_buffer("w3_utower", torch.cat([p[0] for p in w3]).contiguous())
+                self.register_buffer("w3_stower", torch.cat([p[1] for p in w3]).contiguous())
                 c = lambda t: t.detach().float().contiguous().clone()  # noqa: E731
                 heads = [c(f.stem.bias), c(f.policy_conv.weight.view(2, 64)), c(f.policy_conv.bias),
                          c(f.value_conv.weight.view(64)), c(f.value_conv.bias), c(f.value_fc1_wt()),
@@ -495,7 +555,14 @@ class LeafResNet(nn.Module):
             from .engine import load_library
 
             math = net_math() if self.x3 else "f32"
-            if math == "x3" and load_library().bk_leafnet_x3_supported(x.shape[2]):
+            if math == "w3" and load_library().bk_leafnet_w3_supported(x.shape[2]):
+                # the tower as Winograd convolutions on split-f16 MFMA products (bk_leafnet_w3)
+                pf, v = leafnet_w3(x.float().contiguous(), self)
+                if self.features:
+                    return pf, v
+                logits = f.policy_out(pf)
+                return (F.log_softmax(logits, dim=1) if self.normalize else logits), v
+            if math in ("x3", "w3") and load_library().bk_leafnet_x3_supported(x.shape[2]):
                 # the whole net in one launch on split-f16 MFMA products (bk_leafnet_x3)
                 pf, v = leafnet_x3(x.float().contiguous(), self)
                 if self.features:

@@ -348,6 +348,21 @@ int bk_leafnet_x3(const float* obs, int B, int N, int cin, const void* wstem, co
                   const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
                   const float* w2, const float* b2, int P, float* pf, float* vout, float* out, void* stream);
 
+/* The same network and outputs as bk_leafnet_x3 with the residual tower as Winograd F(2x2,3x3)
+ * convolutions on the same split-f16 products (leafnet_w3.hip: 16 products per 2x2 output tile
+ * instead of 36). utower: nlayers x bk_leafnet_w3_weight_bytes() bytes of split U = G g G^T per
+ * conv in the kernel's fragment order (nets.py pack_w3), stower [nlayers][64] its inverse scales;
+ * the stem operands, btower, bounds and the heads as bk_leafnet_x3. x0ws: a workspace of
+ * B x N x N x 64 floats (the stem output, kept for the tower's residual). N = 20
+ * (bk_leafnet_w3_supported), cin = 8, nlayers >= 1. */
+int bk_leafnet_w3_weight_bytes(void);
+int bk_leafnet_w3_supported(int N);
+int bk_leafnet_w3(const float* obs, int B, int N, int cin, const void* wstem, const float* sstem, const float* bstem,
+                  int nlayers, const void* utower, const float* stower, const float* btower, const float* bounds,
+                  const float* wp, const float* bp, const float* wv, const float* bv, const float* w1t, const float* b1,
+                  const float* w2, const float* b2, int P, float* pf, float* vout, float* x0ws, float* out,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

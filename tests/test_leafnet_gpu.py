@@ -115,3 +115,48 @@ def test_leaf_resnet_head_operands_are_buffers():
     assert all(t.device.type == "cpu" for t in cpu.x3_heads) and cpu.x3_wtower.device.type == "cpu"
     back = cpu.to("cuda")
     assert all(t.is_cuda for t in back.x3_heads)
+
+
+@pytest.mark.parametrize("B,nblocks,kind", [(256, 5, "binary"), (7, 2, "dense"), (5, 1, "tiny"), (6, 2, "huge"),
+                                           (3, 3, "binary")])
+def test_leafnet_w3_is_fp32_class(B, nblocks, kind):
+    """bk_leafnet_w3 (the tower as Winograd F(2x2,3x3) on split-f16 products) against the same fp64
+    forward, at the same bar as x3: within 4x the round-1 f32 kernel's error (itself a Winograd
+    tower on the f32 MFMA) or 2e-6 of the output scale, and the tower output within 2e-6."""
+    from blokus_rl_amd.nets import LeafResNet, leafnet_w3, resnet_stem_tower_heads
+
+    N = 20
+    net = _net(N, nblocks, seed=B + 3 * nblocks)
+    g = torch.Generator(device="cuda").manual_seed(B * 5 + nblocks)
+    if kind == "binary":
+        obs = (torch.rand((B, 8, N, N), device="cuda", generator=g) < 0.3).float()
+    else:
+        scale = {"dense": 1.0, "tiny": 1e-3, "huge": 1e3}[kind]
+        obs = torch.randn((B, 8, N, N), device="cuda", generator=g) * scale
+    leaf = LeafResNet(net, normalize=False, features=True).eval()
+    pf, v, out = leafnet_w3(obs, leaf, want_out=True)
+    pf32, v32 = resnet_stem_tower_heads(obs, leaf.w_stem_tower, leaf.u_tower, leaf.b_tower, 2 * nblocks, leaf.f)
+    torch.cuda.synchronize()
+    pf_ref, v_ref, xt_ref = _ref64(net, obs)
+    assert torch.isfinite(pf).all() and torch.isfinite(v).all()
+    e_w3, e_32 = _rel(pf, pf_ref), _rel(pf32, pf_ref)
+    assert e_w3 <= max(4 * e_32, 2e-6), (e_w3, e_32)
+    ev_w3, ev_32 = float((v.double() - v_ref).abs().max()), float((v32.double() - v_ref).abs().max())
+    assert ev_w3 <= max(4 * ev_32, 2e-6), (ev_w3, ev_32)
+    assert _rel(out, xt_ref) <= 2e-6
+
+
+def test_leafnet_w3_outputs_do_not_depend_on_the_batch(monkeypatch):
+    """One workgroup per board: a board's w3 outputs are the same alone and in a batch of 256, and
+    BK_NET_MATH=w3 routes LeafResNet through bk_leafnet_w3."""
+    from blokus_rl_amd.nets import LeafResNet, leafnet_w3
+
+    net = _net(20, 2, seed=12)
+    leaf = LeafResNet(net, normalize=False, features=True).eval()
+    obs = (torch.rand((256, 8, 20, 20), device="cuda") < 0.3).float()
+    pf, v = leafnet_w3(obs, leaf)
+    pf1, v1 = leafnet_w3(obs[200:201].contiguous(), leaf)
+    assert torch.equal(pf[200:201], pf1) and torch.equal(v[200:201], v1)
+    monkeypatch.setenv("BK_NET_MATH", "w3")
+    pfl, vl = leaf(obs)
+    assert torch.equal(pfl, pf) and torch.equal(vl, v)

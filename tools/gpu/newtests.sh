@@ -1,8 +1,7 @@
 #!/bin/bash
-# Quick GPU run of a list of test files (default: the tests touched this session).
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-T=${TESTS:-"tests/test_mcts_gpu.py tests/test_leafnet_gpu.py tests/test_dist_gpu.py tests/test_dropin_gpu.py tests/test_selfplay_gpu.py"}
-timeout -k 10 500 python -u -m pytest $T -m gpu -x -v --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_new.log 2>&1
-rc=$?; echo "pytest rc=$rc"; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_new.log | tail -40
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_search_parity_gpu.py tests/test_vecenv_gpu.py tests/test_selfplay_gpu.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/newtests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/newtests.log
 exit $rc
