@@ -54,6 +54,52 @@ __host__ __device__ constexpr int w3_write_unit(int g) {
 
 __device__ __forceinline__ int w3_swz(int C) { return ((C - 1) >> 1) & 7; }
 
+#ifndef BK_W3_B8
+#define BK_W3_B8 1  // unit barriers leave the 8 grid reads of the V after next in flight
+#endif
+
+#if BK_LN_STAMP
+// timing diagnostics only (make w3stamps): per-wave s_memtime stamps of one launch, tools/w3/stamps_w3.py
+__device__ unsigned long long g_w3_stamps[256 * 4 * 64];
+#define W3STAMP(i)                                                                                         \
+  do {                                                                                                     \
+    if (l == 0 && blockIdx.x < 256) g_w3_stamps[(blockIdx.x * 4 + wave) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define W3STAMP(i) \
+  do {             \
+  } while (0)
+#endif
+
+// f32 adds / subtracts and the f16 split as volatile asm: the unit's VALU work stays spread
+// between its MFMA triples in the order written. Scalar ops, not v_pk_add_f32: beside MFMAs a
+// packed f32 op costs several times the issue slots of the two scalar ops it replaces
+// (MI355X_MICROARCH.md, per-instruction constants: "packed f32 VALU ... an anti-lever beside MFMAs").
+__device__ __forceinline__ float vadd(float a, float b) {
+  float r;
+  asm volatile("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vsub(float a, float b) {
+  float r;
+  asm volatile("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f32x4 vadd4(f32x4 a, f32x4 b) {
+  return f32x4{vadd(a.x, b.x), vadd(a.y, b.y), vadd(a.z, b.z), vadd(a.w, b.w)};
+}
+__device__ __forceinline__ f32x4 vsub4(f32x4 a, f32x4 b) {
+  return f32x4{vsub(a.x, b.x), vsub(a.y, b.y), vsub(a.z, b.z), vsub(a.w, b.w)};
+}
+__device__ __forceinline__ void vsplit2(float x0, float x1, unsigned& hi, unsigned& lo) {
+  asm volatile(
+      "v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+      "v_fma_mixlo_f16 %1, -%0, 1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%0, 1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(x0), "v"(x1));
+}
+
 template <int NACC>
 __device__ __forceinline__ void w3_drain(f32x4 (&acc)[NACC]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -89,6 +135,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int oc = 16 * wave + 4 * ks;
   const size_t b = blockIdx.x;
+  W3STAMP(0);
 
   const __amdgpu_buffer_rsrc_t urs = ln_rsrc(ut, (unsigned)nlayers * kW3UConv);
   const int uvo = l * 16;
@@ -228,6 +275,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
     __syncthreads();
     max_in = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     ex = ex0;
+    W3STAMP(1);
   }
 
   // ---- the V producer: thread = (tile slot pn, channel quad q) of a group (lane groups of the
@@ -252,32 +300,45 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
     }
   };
   auto rd = [&](int va, int k) { return *reinterpret_cast<const f32x4*>(lds + va + k * kW3RowB); };
-  // V[eta] of one transform row from t (the row combination of the window's 4 columns), split and
-  // written to ring slot `slot`
-  auto put_row = [&](const f32x4 (&t)[4], int slot) {
-    const f32x4 v[4] = {sub4(t[0], t[2]), add4(t[1], t[2]), sub4(t[2], t[1]), sub4(t[1], t[3])};
+  // grid reads of V(g, xi): window rows r0, r1 of the 4 columns (B^T row xi = d0 - d2, d1 + d2,
+  // d2 - d1, d1 - d3), issued one unit ahead of the unit that builds V
+  auto fetch = [&](int xi, const int (&va)[4], f32x4 (&dq)[8]) {
+    const int r0 = xi == 0 ? 0 : 1, r1 = xi == 0 ? 2 : (xi == 3 ? 3 : 2);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int k = 0; k < 4; ++k) {
+      dq[2 * k] = rd(va[k], r0);
+      dq[2 * k + 1] = rd(va[k], r1);
+    }
+  };
+  // building V(u) from its reads, in 8 pieces that ride between the 8 MFMA triples of a unit:
+  // 0, 1: the row combinations t of columns 0-1, 2-3; 2, 3: the column combinations v[0..1],
+  // v[2..3]; 4..7: split v[e] and store it to ring slot `slot`. Volatile asm keeps each piece
+  // where it is placed (the compiler would otherwise gather them into one VALU block).
+  struct Prod {
+    f32x4 t[4], v[4];
+  };
+  auto piece = [&](int i, int xi, const f32x4 (&dq)[8], Prod& pr, int slot) {
+    if (i < 2) {
+#pragma unroll
+      for (int k = 2 * i; k < 2 * i + 2; ++k) {
+        const f32x4 a = dq[2 * k], c = dq[2 * k + 1];
+        pr.t[k] = xi == 1 ? vadd4(a, c) : (xi == 2 ? vsub4(c, a) : vsub4(a, c));
+      }
+    } else if (i == 2) {
+      pr.v[0] = vsub4(pr.t[0], pr.t[2]);
+      pr.v[1] = vadd4(pr.t[1], pr.t[2]);
+    } else if (i == 3) {
+      pr.v[2] = vsub4(pr.t[2], pr.t[1]);
+      pr.v[3] = vsub4(pr.t[1], pr.t[3]);
+    } else {
+      const int e = i - 4;
       unsigned h0, h1, l0, l1;
-      split2(v[e].x, v[e].y, h0, l0);
-      split2(v[e].z, v[e].w, h1, l1);
+      vsplit2(pr.v[e].x, pr.v[e].y, h0, l0);
+      vsplit2(pr.v[e].z, pr.v[e].w, h1, l1);
       unsigned char* d = lds + slot * kW3UnitB + vw + e * 4096;
       *reinterpret_cast<u32x2*>(d) = u32x2{h0, h1};
       *reinterpret_cast<u32x2*>(d + 1024) = u32x2{l0, l1};
     }
-  };
-  // V of unit (g, xi) into ring slot `slot`: B^T rows xi = d0 - d2, d1 + d2, d2 - d1, d1 - d3
-  auto produce = [&](int g, int xi, int slot, int pnx) {
-    int va[4];
-    win_cols(g, pnx, va);
-    const int r0 = xi == 0 ? 0 : 1, r1 = xi == 0 ? 2 : (xi == 3 ? 3 : 2);
-    f32x4 t[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const f32x4 a = rd(va[k], r0), c = rd(va[k], r1);
-      t[k] = xi == 1 ? add4(a, c) : (xi == 2 ? sub4(c, a) : sub4(a, c));
-    }
-    put_row(t, slot);
   };
 
   // ---- the output side: lane (wave, l) holds output channels oc..oc+3 of tile slot n
@@ -314,77 +375,25 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
       *reinterpret_cast<f32x4*>(d + kW3RowB) = yy[2];
       *reinterpret_cast<f32x4*>(d + kW3RowB + kW3Pix) = yy[3];
     };
-    produce(0, 0, 0, pn);
+    if (layer == 1) W3STAMP(2);
+    // V(0, 0) up front (its piece order without MFMAs), and the reads of V(0, 1)
+    f32x4 dq[8];
+    int vacur[4], vanext[4];  // window columns of this group's tiles and (from xi = 2 on) the next's
+    win_cols(0, pn, vacur);
+    {
+      Prod pr;
+      fetch(0, vacur, dq);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) piece(i, 0, dq, pr, 0);
+      fetch(1, vacur, dq);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this conv's U (direct-to-AGPR loads)
-#pragma unroll
-    for (int g = 0; g < kW3Groups; ++g) {
-      int pnx = pn, nx = n;
-      asm volatile("" : "+v"(pnx), "+v"(nx));
-      f32x4 xr[4];  // last conv: x0 of the group's outputs
-      if (last) {
-        const int px = out_pixel(g, nx);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) xr[a] = *reinterpret_cast<const f32x4*>(x0b + (px + (a >> 1) * N + (a & 1)) * 64 + oc);
-      }
-#pragma unroll
-      for (int xi = 0; xi < 4; ++xi) {
-        const int u = 4 * g + xi, slot = u & 1;
-        __syncthreads();
-        // the groups whose outputs may now overwrite the grid
-#pragma unroll
-        for (int gw = 0; gw < kW3Groups - 1; ++gw)
-          if (w3_write_unit(gw) == u && 4 * gw + 4 <= u) write_out(gw, y[gw], nx);
-        // B fragments of the unit's 4 positions (2 chunks, hi/lo), one position ahead
-        const unsigned char* rbase = lds + slot * kW3UnitB + vr;
-        h16x8 bf[2][2][2];
-        auto bload = [&](int e) {
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-              bf[e & 1][c][h] = *reinterpret_cast<const h16x8*>(rbase + e * 4096 + c * 2048 + h * 1024);
-        };
-        bload(0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int p = 4 * xi + e;
-          if (e < 3) bload(e + 1);
-          const h16x8(&B)[2][2] = bf[e & 1];
-          asm volatile(
-              "v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\t"
-              "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
-              "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
-              : "=&v"(acc[p])
-              : "a"(U[p][0][0]), "v"(B[0][0]), "a"(U[p][0][1]), "v"(B[0][1]));
-          asm volatile(
-              "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
-              "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
-              "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
-              : "+v"(acc[p])
-              : "a"(U[p][1][0]), "v"(B[1][0]), "a"(U[p][1][1]), "v"(B[1][1]));
-          if (e == 1 && u + 1 < 4 * kW3Groups) produce((u + 1) >> 2, (u + 1) & 3, slot ^ 1, pnx);
-        }
-        // the last group: this unit's positions are done with U -> the next conv's
-        if (g == kW3Groups - 1 && !last) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-              for (int h = 0; h < 2; ++h) U[4 * xi + e][c][h] = w3_uload(urs, uvo, usoff(layer + 1, 4 * xi + e, c, h));
-        }
-      }
-      // ---- the group's epilogue: Y = A^T M A per channel, y = Y s + b (+ x0), ReLU
-      w3_drain(acc);
-      f32x4 z0[4], z1[4];
-#pragma unroll
-      for (int xi = 0; xi < 4; ++xi) {
-        z0[xi] = add4(add4(acc[4 * xi], acc[4 * xi + 1]), acc[4 * xi + 2]);
-        z1[xi] = sub4(sub4(acc[4 * xi + 1], acc[4 * xi + 2]), acc[4 * xi + 3]);
-      }
-      const f32x4 Y[4] = {add4(add4(z0[0], z0[1]), z0[2]), add4(add4(z1[0], z1[1]), z1[2]),
-                          sub4(sub4(z0[1], z0[2]), z0[3]), sub4(sub4(z1[1], z1[2]), z1[3])};
-      const bool ok = tile_ok(g);
+    if (layer == 1) W3STAMP(3);
+    f32x4 Yp[4];  // the previous group's output transform (its epilogue runs in the next unit)
+    f32x4 xr[4];  // last conv: x0 of the previous group's outputs
+    // the epilogue of group gp from its transform Y: y = Y s + b (+ x0), ReLU, the board maximum
+    auto finish = [&](int gp, const f32x4 (&Y)[4]) {
+      const bool ok = tile_ok(gp);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         f32x2 y01 = pk_fma(f32x2{Y[a].x, Y[a].y}, s01, b01);
@@ -396,25 +405,151 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
         y01 = f32x2{max_bits(y01.x, floor), max_bits(y01.y, floor)};
         y23 = f32x2{max_bits(y23.x, floor), max_bits(y23.y, floor)};
         if (ok) mx = max3_abs(max3_abs(mx, y01.x, y01.y), y23.x, y23.y);
-        y[g][a] = f32x4{y01.x, y01.y, y23.x, y23.y};
+        y[gp][a] = f32x4{y01.x, y01.y, y23.x, y23.y};
       }
-      if (last && xout && ok) {
-        const int px = out_pixel(g, nx);
+    };
+    // stage xi of the output transform (Z = M A for transform row xi, then Y += A^T[.][xi] Z)
+    auto zstage = [&](int xi, f32x4 (&Y)[4]) {
+      const f32x4 z0 = vadd4(vadd4(acc[4 * xi], acc[4 * xi + 1]), acc[4 * xi + 2]);
+      const f32x4 z1 = vsub4(vsub4(acc[4 * xi + 1], acc[4 * xi + 2]), acc[4 * xi + 3]);
+      if (xi == 0) {
+        Y[0] = z0;
+        Y[1] = z1;
+      } else if (xi == 1) {
+        Y[0] = vadd4(Y[0], z0);
+        Y[1] = vadd4(Y[1], z1);
+        Y[2] = z0;
+        Y[3] = z1;
+      } else if (xi == 2) {
+        Y[0] = vadd4(Y[0], z0);
+        Y[1] = vadd4(Y[1], z1);
+        Y[2] = vsub4(Y[2], z0);
+        Y[3] = vsub4(Y[3], z1);
+      } else {
+        Y[2] = vsub4(Y[2], z0);
+        Y[3] = vsub4(Y[3], z1);
+      }
+    };
+    f32x4 Yc[4];  // this group's transform
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-          *reinterpret_cast<f32x4*>(xout + (b * NN + px + (a >> 1) * N + (a & 1)) * 64 + oc) = y[g][a];
+    for (int g = 0; g < kW3Groups; ++g) {
+      int pnx = pn, nx = n;
+      asm volatile("" : "+v"(pnx), "+v"(nx));
+#pragma unroll
+      for (int xi = 0; xi < 4; ++xi) {
+        const int u = 4 * g + xi, slot = u & 1;
+        const bool more = u + 1 < 4 * kW3Groups;  // a next unit to build V for
+        if (layer == 1) W3STAMP(4 + u);
+        // the barrier: the V stores of this unit's slot done (all but the 8 grid reads of the
+        // V after next, issued last, which may stay in flight across it)
+        if (!BK_W3_B8 || u == 0 || u + 1 >= 4 * kW3Groups)
+          __syncthreads();
+        else
+          asm volatile("s_waitcnt lgkmcnt(8)\n\ts_barrier" ::: "memory");
+        if (layer == 1) W3STAMP(32 + u);
+        if (xi == 0 && g > 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) vacur[k] = vanext[k];
+        }
+        if (xi == 2 && g + 1 < kW3Groups) win_cols(g + 1, pnx, vanext);
+        // the groups whose outputs may now overwrite the grid (epilogue done in an earlier unit)
+#pragma unroll
+        for (int gw = 0; gw < kW3Groups - 1; ++gw)
+          if (w3_write_unit(gw) == u && 4 * gw + 4 < u) write_out(gw, y[gw], nx);
+        // B fragments of the unit's 4 positions (2 chunks, hi/lo), one position ahead
+        const unsigned char* rbase = lds + slot * kW3UnitB + vr;
+        h16x8 bf[2][2][2];
+        auto bload = [&](int e) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              bf[e & 1][c][h] = *reinterpret_cast<const h16x8*>(rbase + e * 4096 + c * 2048 + h * 1024);
+        };
+        bload(0);
+        Prod pr;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int e = i >> 1, c = i & 1, p = 4 * xi + e;
+          if (c == 0 && e < 3) bload(e + 1);
+          const h16x8(&B)[2] = bf[e & 1][c];
+          if (c == 0)
+            asm volatile(
+                "v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\t"
+                "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
+                "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
+                : "=&v"(acc[p])
+                : "a"(U[p][0][0]), "v"(B[0]), "a"(U[p][0][1]), "v"(B[1]));
+          else
+            asm volatile(
+                "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
+                "v_mfma_f32_16x16x32_f16 %0, %3, %2, %0\n\t"
+                "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
+                : "+v"(acc[p])
+                : "a"(U[p][1][0]), "v"(B[0]), "a"(U[p][1][1]), "v"(B[1]));
+          // the next unit's V, one piece per triple
+          if (more) piece(i, (u + 1) & 3, dq, pr, slot ^ 1);
+          // the output transform of the previous unit's transform row (this group), or of the
+          // previous group's last row + its epilogue (at xi = 0), in the unit's second half
+          if (i == 4) {
+            if (xi > 0) zstage(xi - 1, Yc);
+            else if (g > 0) zstage(3, Yp);
+          }
+          if (i == 6 && xi == 0 && g > 0) {
+            finish(g - 1, Yp);
+            // a group whose pixels are already dead (write unit = this one) goes out right away
+            if (w3_write_unit(g - 1) == u) write_out(g - 1, y[g - 1], nx);
+            if (last && xout && tile_ok(g - 1)) {
+              const int px = out_pixel(g - 1, nx);
+#pragma unroll
+              for (int a = 0; a < 4; ++a)
+                *reinterpret_cast<f32x4*>(xout + (b * NN + px + (a >> 1) * N + (a & 1)) * 64 + oc) = y[g - 1][a];
+            }
+          }
+          // the last group: position e is done with U after its second chunk -> the next conv's
+          if (g == kW3Groups - 1 && !last && c == 1) {
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) U[p][cc][h] = w3_uload(urs, uvo, usoff(layer + 1, p, cc, h));
+          }
+        }
+        // the reads of the V after next (built during the next unit)
+        if (u + 2 < 4 * kW3Groups) fetch((u + 2) & 3, xi < 2 ? vacur : vanext, dq);
+        if (xi == 3) {  // this group's transform is complete but for row 3: finished in the next unit
+#pragma unroll
+          for (int a = 0; a < 4; ++a) Yp[a] = Yc[a];
+          if (last) {  // x0 of this group's outputs, for its epilogue in the next unit
+            const int px = out_pixel(g, nx);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) xr[a] = *reinterpret_cast<const f32x4*>(x0b + (px + (a >> 1) * N + (a & 1)) * 64 + oc);
+          }
+        }
       }
-      if (g == kW3Groups - 1) write_out(g, y[g], nx);  // after the layer's last read: no wait
     }
+    // the last group's row 3 and epilogue, then its outputs (after the layer's last read: no wait)
+    w3_drain(acc);
+    zstage(3, Yp);
+    finish(kW3Groups - 1, Yp);
+    if (last && xout && tile_ok(kW3Groups - 1)) {
+      const int px = out_pixel(kW3Groups - 1, n);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        *reinterpret_cast<f32x4*>(xout + (b * NN + px + (a >> 1) * N + (a & 1)) * 64 + oc) = y[kW3Groups - 1][a];
+    }
+    write_out(kW3Groups - 1, y[kW3Groups - 1], n);
     // the board maximum of this conv's output (the next conv's bound), then the next conv
+    if (layer == 1) W3STAMP(60);
     mx = wave_max_f(mx);
     if (l == 0) red[4 + 4 * (layer & 1) + wave] = mx;
     __syncthreads();
+    if (layer == 1) W3STAMP(61);
     max_in = fmaxf(fmaxf(red[4 + 4 * (layer & 1)], red[5 + 4 * (layer & 1)]),
                    fmaxf(red[6 + 4 * (layer & 1)], red[7 + 4 * (layer & 1)]));
     ex = ex_out;
   }
 
+  W3STAMP(62);
   // ---- heads (blokus_nnet.py:146-150, BN folded) from the tower output in the grid: wave w takes
   // channels 16w..16w+15 of pixel p (lane), the 4 waves' partials meet in LDS (the dead V ring)
   float* hp = reinterpret_cast<float*>(lds);  // [NN][4 waves][3]
@@ -493,6 +628,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
       }
     }
   }
+  W3STAMP(63);
 }
 
 }  // namespace
@@ -503,6 +639,12 @@ using namespace bk;
 extern "C" {
 
 int bk_leafnet_w3_supported(int N) { return N == kW3N; }
+
+#if BK_LN_STAMP
+int bk_w3_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w3_stamps), sizeof(g_w3_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int bk_leafnet_w3_weight_bytes(void) { return kW3UConv; }
 
