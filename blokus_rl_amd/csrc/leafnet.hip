@@ -47,7 +47,9 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned char* act = lds;                  // 16 planes [hi q | lo q][(N+2) x RS slots][16 B]
   unsigned char* sin = lds + 16 * PL;        // 2 planes: the stem input hi, lo
-  float* red = reinterpret_cast<float*>(lds + 18 * PL);
+  float* red = reinterpret_cast<float*>(lds + ln_lds_body(N));
+  constexpr int X0L = ln_x0_lds_groups(N);   // x0 groups 0..X0L-1 stashed in LDS
+  f32x4* x0s = reinterpret_cast<f32x4*>(lds + 16 * PL);
   const int tid = threadIdx.x, l = tid & 63, n = l & 15, ks = l >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
   const int oc = 16 * wave + 4 * ks;  // the lane's 4 output channels oc..oc+3 in the D fragments
@@ -279,11 +281,16 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
 #if BK_LN_X0A
     // x0 waits out the tower in AGPRs (read once, by the last conv): its VGPRs go to the loop
 #pragma unroll
-    for (int g = 0; g < NG; ++g) asm volatile("" : "+a"(x0[g]));
+    for (int g = X0L; g < NG; ++g) asm volatile("" : "+a"(x0[g]));
 #endif
     post_max(mx, 0);
-    __syncthreads();  // the stem's input planes are a separate region: nothing else to wait for
+    __syncthreads();  // every wave is done with the stem's input planes (the x0 stash reuses them)
     write_act();
+#pragma unroll
+    for (int g = 0; g < X0L; ++g) {
+      x0s[g * kLnThreads + tid] = x0[g];
+      x0[g] = f32x4{0.f, 0.f, 0.f, 0.f};  // not kept in registers
+    }
     __syncthreads();
     max_in = board_max(0);
     ex = ex_out;
@@ -346,6 +353,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       max_in = board_max((layer + 1) & 1);
       ex = ex_out;
     } else {
+#pragma unroll
+      for (int g = 0; g < X0L; ++g) x0[g] = x0s[g * kLnThreads + tid];
       epilogue(sv, bv, true, true, x0, false, 0);
     }
     if (layer < 8) LNSTAMP(5 + 2 * layer, __builtin_amdgcn_s_memtime());

@@ -82,8 +82,17 @@ __host__ __device__ constexpr int ln_groups(int N) { return ((N * N + 15) / 16 +
 // input (8 channels) takes two more planes (hi, lo).
 __host__ __device__ constexpr int ln_row(int N) { return N == 14 ? 18 : N + 2; }  // slot classes mod 16 balanced
 __host__ __device__ constexpr int ln_plane(int N) { return ((N + 2) * ln_row(N) * 16 + 255) / 256 * 256; }
-// LDS bytes of k_leafnet_x3<N>: 16 activation planes, 2 stem planes, wave maxima (2 x 4 + 4)
-__host__ __device__ constexpr int ln_lds_bytes(int N) { return 18 * ln_plane(N) + 64; }
+// The stem output's groups that wait out the tower in LDS instead of registers (k_leafnet_x3<20>:
+// the register file holds the other 18 groups; all 25 would spill 26 registers to scratch), in the
+// stem planes' region (dead after the stem) and above it: [group][256 threads] x 16 B
+__host__ __device__ constexpr int ln_x0_lds_groups(int N) { return N == 20 ? 7 : 0; }
+// LDS bytes of k_leafnet_x3<N>: 16 activation planes, then the 2 stem planes or the x0 stash
+// (whichever is larger), then the wave maxima (2 x 4 + 4 floats)
+__host__ __device__ constexpr int ln_lds_body(int N) {
+  return 16 * ln_plane(N) + (2 * ln_plane(N) > ln_x0_lds_groups(N) * 256 * 16 ? 2 * ln_plane(N)
+                                                                                 : ln_x0_lds_groups(N) * 256 * 16);
+}
+__host__ __device__ constexpr int ln_lds_bytes(int N) { return ln_lds_body(N) + 64; }
 
 // The board's pixels in MFMA columns: slot (g, n) of pixel group g, column n. Any bijection works
 // (reads and writes use the same map); this one gives each group 16 pixels whose grid slots are

@@ -60,10 +60,10 @@ __device__ __forceinline__ int w3_swz(int C) { return ((C - 1) >> 1) & 7; }
 
 #if BK_LN_STAMP
 // timing diagnostics only (make w3stamps): per-wave s_memtime stamps of one launch, tools/w3/stamps_w3.py
-__device__ unsigned long long g_w3_stamps[256 * 4 * 64];
+__device__ unsigned long long g_w3_stamps[256 * 4 * 128];
 #define W3STAMP(i)                                                                                         \
   do {                                                                                                     \
-    if (l == 0 && blockIdx.x < 256) g_w3_stamps[(blockIdx.x * 4 + wave) * 64 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (l == 0 && blockIdx.x < 256) g_w3_stamps[(blockIdx.x * 4 + wave) * 128 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define W3STAMP(i) \
@@ -391,11 +391,12 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
     if (layer == 1) W3STAMP(3);
     f32x4 Yp[4];  // the previous group's output transform (its epilogue runs in the next unit)
     f32x4 xr[4];  // last conv: x0 of the previous group's outputs
-    // the epilogue of group gp from its transform Y: y = Y s + b (+ x0), ReLU, the board maximum
-    auto finish = [&](int gp, const f32x4 (&Y)[4]) {
+    // the epilogue of group gp from its transform Y, subpixels a0..a1-1: y = Y s + b (+ x0),
+    // ReLU, the board maximum
+    auto finish = [&](int gp, const f32x4 (&Y)[4], int a0, int a1) {
       const bool ok = tile_ok(gp);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
+      for (int a = a0; a < a1; ++a) {
         f32x2 y01 = pk_fma(f32x2{Y[a].x, Y[a].y}, s01, b01);
         f32x2 y23 = pk_fma(f32x2{Y[a].z, Y[a].w}, s23, b23);
         if (last) {
@@ -408,11 +409,15 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
         y[gp][a] = f32x4{y01.x, y01.y, y23.x, y23.y};
       }
     };
-    // stage xi of the output transform (Z = M A for transform row xi, then Y += A^T[.][xi] Z)
-    auto zstage = [&](int xi, f32x4 (&Y)[4]) {
-      const f32x4 z0 = vadd4(vadd4(acc[4 * xi], acc[4 * xi + 1]), acc[4 * xi + 2]);
-      const f32x4 z1 = vsub4(vsub4(acc[4 * xi + 1], acc[4 * xi + 2]), acc[4 * xi + 3]);
-      if (xi == 0) {
+    // the output transform of transform row xi in three parts: Z = M A (z0 = M0 + M1 + M2,
+    // z1 = M1 - M2 - M3), then Y += A^T[.][xi] Z
+    f32x4 z0, z1;
+    auto zpart = [&](int part, int xi, f32x4 (&Y)[4]) {
+      if (part == 0) {
+        z0 = vadd4(vadd4(acc[4 * xi], acc[4 * xi + 1]), acc[4 * xi + 2]);
+      } else if (part == 1) {
+        z1 = vsub4(vsub4(acc[4 * xi + 1], acc[4 * xi + 2]), acc[4 * xi + 3]);
+      } else if (xi == 0) {
         Y[0] = z0;
         Y[1] = z1;
       } else if (xi == 1) {
@@ -467,7 +472,18 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
               bf[e & 1][c][h] = *reinterpret_cast<const h16x8*>(rbase + e * 4096 + c * 2048 + h * 1024);
         };
         bload(0);
+        // the unit's schedule: V pieces 0-1 under the B fragments' LDS latency, then after
+        // triple i piece i + 2, the output transform of the previous row in three parts (after
+        // triples 2-4), and at xi = 0 the previous group's epilogue (after triples 5-6)
         Prod pr;
+        constexpr int kSt = -1;
+        const int su = (u == 9 ? 64 : (u == 12 ? 80 : (u == 10 ? 96 : kSt)));
+        if (layer == 1 && su >= 0) W3STAMP(su);
+        if (more) {
+          piece(0, (u + 1) & 3, dq, pr, slot ^ 1);
+          piece(1, (u + 1) & 3, dq, pr, slot ^ 1);
+        }
+        if (layer == 1 && su >= 0) W3STAMP(su + 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int e = i >> 1, c = i & 1, p = 4 * xi + e;
@@ -487,16 +503,14 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
                 "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
                 : "+v"(acc[p])
                 : "a"(U[p][1][0]), "v"(B[0]), "a"(U[p][1][1]), "v"(B[1]));
-          // the next unit's V, one piece per triple
-          if (more) piece(i, (u + 1) & 3, dq, pr, slot ^ 1);
-          // the output transform of the previous unit's transform row (this group), or of the
-          // previous group's last row + its epilogue (at xi = 0), in the unit's second half
-          if (i == 4) {
-            if (xi > 0) zstage(xi - 1, Yc);
-            else if (g > 0) zstage(3, Yp);
+          if (layer == 1 && su >= 0) W3STAMP(su + 2 + i);  // after triple i
+          if (more && i + 2 < 8) piece(i + 2, (u + 1) & 3, dq, pr, slot ^ 1);
+          if (i >= 2 && i <= 4) {
+            if (xi > 0) zpart(i - 2, xi - 1, Yc);
+            else if (g > 0) zpart(i - 2, 3, Yp);
           }
+          if ((i == 5 || i == 6) && xi == 0 && g > 0) finish(g - 1, Yp, i == 5 ? 0 : 2, i == 5 ? 2 : 4);
           if (i == 6 && xi == 0 && g > 0) {
-            finish(g - 1, Yp);
             // a group whose pixels are already dead (write unit = this one) goes out right away
             if (w3_write_unit(g - 1) == u) write_out(g - 1, y[g - 1], nx);
             if (last && xout && tile_ok(g - 1)) {
@@ -514,8 +528,10 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
               for (int h = 0; h < 2; ++h) U[p][cc][h] = w3_uload(urs, uvo, usoff(layer + 1, p, cc, h));
           }
         }
+        if (layer == 1 && su >= 0) W3STAMP(su + 10);
         // the reads of the V after next (built during the next unit)
         if (u + 2 < 4 * kW3Groups) fetch((u + 2) & 3, xi < 2 ? vacur : vanext, dq);
+        if (layer == 1 && su >= 0) W3STAMP(su + 11);
         if (xi == 3) {  // this group's transform is complete but for row 3: finished in the next unit
 #pragma unroll
           for (int a = 0; a < 4; ++a) Yp[a] = Yc[a];
@@ -529,8 +545,9 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
     }
     // the last group's row 3 and epilogue, then its outputs (after the layer's last read: no wait)
     w3_drain(acc);
-    zstage(3, Yp);
-    finish(kW3Groups - 1, Yp);
+#pragma unroll
+    for (int part = 0; part < 3; ++part) zpart(part, 3, Yp);
+    finish(kW3Groups - 1, Yp, 0, 4);
     if (last && xout && tile_ok(kW3Groups - 1)) {
       const int px = out_pixel(kW3Groups - 1, n);
 #pragma unroll

@@ -25,9 +25,9 @@ for _ in range(5):
 torch.cuda.synchronize()
 lib = load_library()
 lib.bk_w3_stamps.argtypes = [ctypes.c_void_p]
-s = np.zeros(256 * 4 * 64, dtype=np.uint64)
+s = np.zeros(256 * 4 * 128, dtype=np.uint64)
 assert lib.bk_w3_stamps(s.ctypes.data_as(ctypes.c_void_p)) == 0
-s = s.reshape(256, 4, 64).astype(np.int64)
+s = s.reshape(256, 4, 128).astype(np.int64)
 rel = s - s[:, :, 0:1]
 med = lambda x: float(np.median(x))  # noqa: E731
 res = {"total": med(rel[:, :, 63]), "stem": med(rel[:, :, 1]), "layer0_and_1_to_start": med(rel[:, :, 2] - rel[:, :, 1]),
@@ -46,4 +46,9 @@ res["tower_end"] = med(rel[:, :, 62])
 res["heads"] = med(rel[:, :, 63] - rel[:, :, 62])
 res["sum_issue"] = sum(x["issue"] for x in units)
 res["sum_barrier"] = sum(x["barrier_wait"] for x in units)
+# inside units 9, 10, 12 of layer 1: after the barrier -> V pieces 0-1 -> triple 0..7 -> fetch
+for u, base in ((9, 64), (10, 96), (12, 80)):
+    marks = [rel[:, :, 32 + u]] + [rel[:, :, base + j] for j in range(12)]
+    names = ["write_out+bload0", "pieces01"] + [f"triple{i}+piece" for i in range(8)] + ["tail", "fetch"]
+    res[f"unit{u}_inside"] = {nm: med(marks[j + 1] - marks[j]) for j, nm in enumerate(names)}
 print(json.dumps(res))
