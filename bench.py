@@ -177,10 +177,11 @@ def bench_dry(args, world, rank):
             "backend": dist.get_backend() if dist_active() else None}
 
 
-def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
-    if one exists for this kernel; FETCH_SIZE doubled per the gfx950 correction
-    (MI355X_MICROARCH.md §HBM). None when absent."""
+def _pmc_traffic(kernel_prefix: str, units_per_launch: int, with_source: bool = False):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json) of this
+    kernel at this launch size, FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md
+    §HBM); the newest file (by name: rNN_ prefix) wins. None when absent. with_source: (bytes,
+    the profile's file name) — a committed measurement, not one of this run."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for fp in reversed(files):
         try:
@@ -188,10 +189,11 @@ def _pmc_traffic(kernel_prefix: str, units_per_launch: int):
                 d = json.load(f)
             k = d.get("kernels", {}).get(kernel_prefix)
             if k and k.get("units_per_launch") == units_per_launch:
-                return float(k["hbm_bytes_per_launch"])
+                v = float(k["hbm_bytes_per_launch"])
+                return (v, os.path.basename(fp)) if with_source else v
         except Exception:
             continue
-    return None
+    return (None, None) if with_source else None
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -381,7 +383,7 @@ def bench_legal(args, world, rank):
     boards_total = B * steps_done * world
     value = boards_total / elapsed
     achieved = LEGAL_BYTES_PER_BOARD * B / (kernel_ms * 1e-3)
-    traffic = _pmc_traffic("k_legal_mask", B)
+    traffic, traffic_src = _pmc_traffic("k_legal_mask", B, with_source=True)
     out = {
         "metric": "legal-move boards/sec (20x20, 4 players, 30433-id bitmask)",
         "value": value,
@@ -399,7 +401,7 @@ def bench_legal(args, world, rank):
                    "global_batch": B * world, "parallelism": f"dp{world} (independent shards)",
                    "graph": bool(args.graph)},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_legal_mask", "kernel_ms": kernel_ms,
                      "bytes_per_unit": LEGAL_BYTES_PER_BOARD, "units_per_launch": B},
     }
@@ -483,9 +485,16 @@ def bench_vecenv(args, world, rank):
     torch.cuda.synchronize()
     dt2 = time.perf_counter() - t1
     achieved = VEC_BYTES_PER_STEP * E / (kernel_ms * 1e-3)
-    out = {"metric": "PPO vector-env steps/sec (7x7, 2 players, 919 ids, random opponent)",
+    # the headline is the DEVICE rate (graph-replayed launches, in-kernel agent draws); a gym-style
+    # loop calling env.step() per step gets eager_env_step_calls (one launch + tensor bookkeeping
+    # per call), and a PPO loop sampling from masked logits with_masked_policy_sampling
+    out = {"metric": "PPO vector-env device steps/sec (7x7, 2 players, 919 ids, random opponent; HIP-graph-replayed "
+                     "k_vec_step7 launches, in-kernel agent draws)",
            "value": E * steps_done * world / dt, "unit": "env-steps/s", "envs_per_gpu": E,
            "steps": steps_done, "eager_env_step_calls": {"value": eager * world, "unit": "env-steps/s"},
+           "byte_accounting": "bytes_per_unit counts the state words a 7x7 game uses (393 B since round 4; "
+                              "round 3 counted the whole 384-B state each way, 965 B): fractions are not "
+                              "comparable with rounds <= 3",
            "with_masked_policy_sampling": {"value": E * n2 / dt2, "unit": "env-steps/s"},
            "roofline": {"bound": "hbm", "kernel": "k_vec_step7", "achieved": achieved / 1e9,
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
@@ -714,15 +723,16 @@ def main():
         if "k_leaf_step" in sr.get("kernel", ""):
             # HBM-side bytes per launch of the search kernel (profiles/*pmc*leafstep*.json) over its
             # live launch time: the fraction of the HBM roofline it actually draws
-            tr = _pmc_traffic("k_leaf_step_ov", args.games)
-            sr["traffic"] = tr
+            # (a committed profile's bytes over this run's time: an estimate, named as one)
+            tr, src = _pmc_traffic("k_leaf_step_ov", args.games, with_source=True)
+            sr["traffic"], sr["traffic_source"] = tr, src
             if tr and sr.get("k_leaf_step_us"):
-                sr["achieved"] = tr / (sr["k_leaf_step_us"] * 1e-6) / 1e9
-                sr["frac"] = sr["achieved"] / sr["peak"]
+                sr["achieved_est"] = tr / (sr["k_leaf_step_us"] * 1e-6) / 1e9
+                sr["frac_est"] = sr["achieved_est"] / sr["peak"]
         kname = out["roofline"].get("kernel", "").split(" ")[0]
         if kname.startswith("k_conv3x3") or kname.startswith("k_tower") or kname.startswith("k_leafnet"):
             # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)
-            out["roofline"]["traffic"] = _pmc_traffic(kname, args.games)
+            out["roofline"]["traffic"], out["roofline"]["traffic_source"] = _pmc_traffic(kname, args.games, True)
         if args.workload == "all" and args.model == "resnet" and args.nn_dtype == "fp32":
             # the same self-play with the leaf net at the reference's own precision: every product
             # on the exact-f32 MFMA (BK_NET_MATH=f32), timed the same way

@@ -280,9 +280,10 @@ def bench_selfplay(args, world, rank):
                   "achieved": None, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": None, "traffic": None,
                   "addressed_bytes_per_sim_step": ls["bytes_per_sim_step"], "addressed_GBps": addressed / 1e9,
                   "search_ms_per_sim_step": ls["ms_per_sim_step"], "k_leaf_step_us": ls["k_leaf_step_us"],
-                  "note": "achieved/frac = HBM-side bytes per k_leaf_step_ov launch (rocprofv3 PMC, "
-                          "FETCH_SIZE x2 + WRITE_SIZE, profiles/*pmc*leafstep*.json) / the live launch time; "
-                          "addressed_* count the bytes as the kernels address them (each W row per use)"}
+                  "note": "achieved_est/frac_est = the HBM-side bytes per k_leaf_step_ov launch of a committed "
+                          "rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE, traffic_source) over this run's live "
+                          "launch time: an estimate, not a measurement of this run; addressed_* count the bytes "
+                          "as the kernels address them (each W row per use)"}
     else:
         sbytes = search_bytes(delta, local_sims, obs_bytes, 8 * eng.W)
         search_ms = ms.get("select", 0.0) + ms.get("expand", 0.0)
