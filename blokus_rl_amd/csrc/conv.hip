@@ -36,13 +36,8 @@ namespace bk {
 namespace {
 
 constexpr int kCout = 64;
-#ifndef BK_CONV_THREADS
-#define BK_CONV_THREADS 768
-#endif
-#ifndef BK_CONV_DB
-#define BK_CONV_DB 8
-#endif
-constexpr int kConvThreads = BK_CONV_THREADS;
+constexpr int kConvThreads = 768;
+constexpr int kConvDB = 8;  // B prefetch distance in k-steps
 constexpr int kConvWaves = kConvThreads / kWave;
 
 template <int VEC>
@@ -88,7 +83,7 @@ __device__ __forceinline__ void conv_run(const float* __restrict__ x, const f32x
   constexpr int S = CIN / 4;
   constexpr int Q = CIN / (4 * VEC);
   constexpr int KS = 9 * S;
-  constexpr int DB = S < BK_CONV_DB ? S : BK_CONV_DB;  // B prefetch distance in k-steps (divides KS)
+  constexpr int DB = S < kConvDB ? S : kConvDB;  // B prefetch distance in k-steps (divides KS)
   static_assert(KS % DB == 0, "ring must wrap at tile boundaries");
   using V = typename VecT<VEC>::T;
   using WT = typename std::conditional<NJ == 4, f32x4, float>::type;
@@ -283,10 +278,7 @@ int launch_conv(const float* x, const f32x4* wp, const float* b, const float* r,
 // halves of a window are fetched into one L2.
 //   KB = 1: 8 waves (2 per SIMD, 256 registers), waves w and w^1 the two blocks of a group.
 //   KB = 2: 4 waves (1 per SIMD, 512 registers), a wave both blocks.
-#ifndef BK_WINO_KB
-#define BK_WINO_KB 1
-#endif
-constexpr int kWinoKB = BK_WINO_KB;
+constexpr int kWinoKB = 1;
 constexpr int kWinoThreads = kWinoKB == 1 ? 512 : 256;
 constexpr int kWinoHalf = 2 * 16 * 16 * kWave;  // floats of U per 32-channel half: [2 blk][16 p][16 s][64]
 

@@ -105,20 +105,14 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // the weights stream through a ring of kLnWpf + 1 chunks, kLnWpf chunks ahead of the MFMAs and
   // on into the next layer (18 chunks per layer: the ring slot of chunk c is c % (kLnWpf + 1) in
   // every layer), so no layer starts on an exposed L2 load
-  static_assert(18 % (kLnWpf + 1) == 0, "BK_LN_WPF: the ring must divide the 18 chunks of a layer");
+  static_assert(18 % (kLnWpf + 1) == 0, "kLnWpf: the ring must divide the 18 chunks of a layer");
   constexpr int kLayerBlocks = 18 * 4 * 2;  // (chunk, wave, part) blocks of 64 x 16 B per layer
-#if BK_LN_WBUF
   const __amdgpu_buffer_rsrc_t wrs = ln_rsrc(wt, (unsigned)nlayers * kLayerBlocks * 1024u);
   // part p (0 hi, 1 lo) of the lane's A fragment of chunk c of tower layer `layer`
   auto wload = [&](int layer, int c, int p) {
     return __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                          wrs, l * 16, ((layer * kLayerBlocks + c * 8 + wave * 2 + p) * 64) * 16, 0));
   };
-#else
-  auto wload = [&](int layer, int c, int p) {
-    return wt[(size_t)layer * kLayerBlocks * 64 + (size_t)(c * 8 + wave * 2 + p) * 64 + l];
-  };
-#endif
   h16x8 wq[kLnWpf + 1][2];  // issued here: in flight under the stem
 #pragma unroll
   for (int c = 0; c < kLnWpf; ++c) {
@@ -220,7 +214,6 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // both lo halves, so each lane stores one 16-B slot (hi plane, or the lo plane next to it).
   auto write_act = [&]() {
     const int o = 2 * wave + (ks >> 1);
-#if BK_LN_WRITE8
     // each lane stores its 4 channels' hi and lo halves (8 B each) into its half of the octet's
     // 16-B slot in the hi plane and in the lo plane (no lane swaps)
     unsigned char* base = act + ((o & 3) * 4 + (o >> 2) * 2) * PL + (ks & 1) * 8;
@@ -232,20 +225,6 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         *reinterpret_cast<u32x2*>(base + slot_b(g) + PL) = u32x2{w.z, w.w};
       }
     }
-#else
-    unsigned char* base = act + ((o & 3) * 4 + (o >> 2) * 2 + (ks & 1)) * PL;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      // bit_cast the whole vector: hipcc's __builtin_bit_cast of an ext_vector element reads
-      // element 0 whatever the index (ROCm 7.2)
-      const u32x4 w = __builtin_bit_cast(u32x4, acc[g]);  // {hi 01, hi 23, lo 01, lo 23}
-      // the swaps in place (the builtin returns copies: 4 moves per group to rebuild the tuple)
-      unsigned x = w.x, y = w.y, z = w.z, t = w.w;
-      asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3"
-          : "+v"(x), "+v"(z), "+v"(y), "+v"(t));
-      if (is_valid(g)) *reinterpret_cast<u32x4*>(base + slot_b(g)) = u32x4{x, y, z, t};
-    }
-#endif
   };
   // the scale of a conv's output from the bound |y| <= A max_in + B (A = the largest row L1 norm
   // of the weights, B = the largest |bias|: nets.pack_x3)
@@ -278,11 +257,9 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
       acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
                      __builtin_bit_cast(float, l1)};
     }
-#if BK_LN_X0A
     // x0 waits out the tower in AGPRs (read once, by the last conv): its VGPRs go to the loop
 #pragma unroll
     for (int g = X0L; g < NG; ++g) asm volatile("" : "+a"(x0[g]));
-#endif
     post_max(mx, 0);
     __syncthreads();  // every wave is done with the stem's input planes (the x0 stash reuses them)
     write_act();

@@ -42,23 +42,8 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 // a chunk load the first kLnPf of the next), so the LDS latency is never exposed at a chunk start.
 // The slot of group g is g % kLnSlots in every chunk, which needs NG % kLnSlots == 0: the board's
 // groups are padded with spare ones (all columns spare: halo reads, no writes) up to a multiple.
-#ifndef BK_LN_X0A
-#define BK_LN_X0A 1  // A/B knob: the stem output x0 in AGPRs through the tower
-#endif
-#ifndef BK_LN_WRITE8
-#define BK_LN_WRITE8 1  // A/B knob: activation stores as two 8-B stores per lane (no lane swaps)
-#endif
-#ifndef BK_LN_WBUF
-#define BK_LN_WBUF 1  // A/B knob: tower weights through buffer loads (SGPR chunk offsets)
-#endif
-#ifndef BK_LN_PF
-#define BK_LN_PF 2  // groups of read-ahead (A/B knob, 1..4)
-#endif
-#ifndef BK_LN_WPF
-#define BK_LN_WPF 1  // chunks of weight read-ahead (A/B knob: 1 or 2)
-#endif
 #ifndef BK_LN_VACC
-#define BK_LN_VACC 0  // A/B knob: the MFMA accumulators in VGPRs (1) or AGPRs (0)
+#define BK_LN_VACC 0  // the MFMA accumulators in VGPRs (1: leafnet_w3.hip, whose AGPRs hold U) or AGPRs (0)
 #endif
 #if BK_LN_VACC
 #define BK_ACC_W "=&v"
@@ -67,8 +52,9 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 #define BK_ACC_W "=&a"
 #define BK_ACC_RW "+a"
 #endif
-constexpr int kLnPf = BK_LN_PF, kLnSlots = 5, kLnWpf = BK_LN_WPF;
-static_assert(kLnPf >= 1 && kLnPf < kLnSlots, "BK_LN_PF");
+// read-ahead: 2 groups of B fragments (4: no gain), 1 chunk of weights (2: no gain)
+constexpr int kLnPf = 2, kLnSlots = 5, kLnWpf = 1;
+static_assert(kLnPf >= 1 && kLnPf < kLnSlots, "kLnPf");
 __host__ __device__ constexpr int ln_groups(int N) { return ((N * N + 15) / 16 + kLnSlots - 1) / kLnSlots * kLnSlots; }
 
 // The layer input in LDS: 16 planes, each a zero-haloed grid of (N+2) rows x ln_row(N) slots of

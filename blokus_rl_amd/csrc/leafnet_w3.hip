@@ -54,10 +54,6 @@ __host__ __device__ constexpr int w3_write_unit(int g) {
 
 __device__ __forceinline__ int w3_swz(int C) { return ((C - 1) >> 1) & 7; }
 
-#ifndef BK_W3_B8
-#define BK_W3_B8 1  // unit barriers leave the 8 grid reads of the V after next in flight
-#endif
-
 #if BK_LN_STAMP
 // timing diagnostics only (make w3stamps): per-wave s_memtime stamps of one launch, tools/w3/stamps_w3.py
 __device__ unsigned long long g_w3_stamps[256 * 4 * 128];
@@ -447,7 +443,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
         if (layer == 1) W3STAMP(4 + u);
         // the barrier: the V stores of this unit's slot done (all but the 8 grid reads of the
         // V after next, issued last, which may stay in flight across it)
-        if (!BK_W3_B8 || u == 0 || u + 1 >= 4 * kW3Groups)
+        if (u == 0 || u + 1 >= 4 * kW3Groups)
           __syncthreads();
         else
           asm volatile("s_waitcnt lgkmcnt(8)\n\ts_barrier" ::: "memory");

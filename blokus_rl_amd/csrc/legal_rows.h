@@ -33,15 +33,6 @@ struct RowCtx {
 // forbidden and anchor accumulators), then legal = anchor & ~forbidden, validity masks, and the
 // W-bit field ORed into the board's LDS bitmask (two 32-bit ORs; the second is 0 unless the field
 // straddles a word).
-#ifndef BK_MASK_SPLIT
-#define BK_MASK_SPLIT 0  // A/B knob: even / odd origin rows in separate LDS atomics (leaf bitmask)
-#endif
-#ifndef BK_MASK_SKIP0
-#define BK_MASK_SKIP0 1  // A/B knob: LDS atomics only for non-zero fields (0: every lane, every word)
-#endif
-#ifndef BK_MASK_DIRECT
-#define BK_MASK_DIRECT 1  // A/B knob: each wave runs only its orientations (orient_dispatch)
-#endif
 // SKIP0: a wave holding ONE board (lanes 0..N-1 its rows, the rest idle) ORs only non-zero fields:
 // otherwise the idle lanes and the empty rows, which all address the word of row 0, serialise on
 // it (the leaf bitmask of the search: 52.7 vs 53.8 us a leaf step). The 3-board legal kernel
@@ -82,7 +73,7 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
       atomicOr(dst + 1, (uint32_t)(x >> 32));
       atomicOr(dst, (uint32_t)x);
     }
-  } else if (SKIP0 && BK_MASK_SKIP0) {
+  } else if (SKIP0) {
     if (v) {
       atomicOr(dst, (uint32_t)x);
       if ((uint32_t)(x >> 32)) atomicOr(dst + 1, (uint32_t)(x >> 32));
@@ -127,7 +118,7 @@ __device__ __forceinline__ void orient_step_at(const DevPreset& dp, const RowCtx
   if (oc.piece >= dp.num_pieces) return;  // wave-uniform
   const int N = dp.N;
   int base = kOrientBase.cnt[O] * N * N + kOrientBase.b[O] * N + kOrientBase.c[O];
-  orient_step<O, 1, BK_MASK_SPLIT, true>(dp, c, 0, base);
+  orient_step<O, 1, 0, true>(dp, c, 0, base);
 }
 template <int W, int WPB, size_t... Ks>
 __device__ __forceinline__ void orient_part(const DevPreset& dp, const RowCtx& c, std::index_sequence<Ks...>) {
@@ -226,11 +217,7 @@ __device__ __forceinline__ void build_mask_rows_wg(const DevPreset& dp, const ui
   BK_MASK_STAMP(5);
   __syncthreads();
   BK_MASK_STAMP(6);
-#if BK_MASK_DIRECT
   orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
-#else
-  orient_all<WPB, 0, true>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
-#endif
   BK_MASK_STAMP(7);
   __syncthreads();
 }
@@ -357,7 +344,6 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32 + (j < bpw ? j : 0) * dp.W32pad;
   __syncthreads();  // mask zeroing complete
-#if BK_MASK_DIRECT
   if constexpr (WPB > 1) {
     // each wave only its own orientations at compile-time bases: orient_all's walk over the
     // other waves' orientations (a scalar branch + base update each) doubled the instruction count
@@ -365,9 +351,6 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   } else {
     orient_all<WPB, SPLIT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
   }
-#else
-  orient_all<WPB, SPLIT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
-#endif
   __syncthreads();
   // stream out every board of the group: 16-B stores when rows are 16-B aligned (W64 even);
   // popcounts accumulate per lane, one wave reduction and one LDS add per board

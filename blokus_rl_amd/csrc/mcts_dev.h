@@ -16,10 +16,7 @@ constexpr int kMaxDepth = 96;
 constexpr int kExpandLdsIds = 2048;  // leaf ids staged in LDS up to this K
 constexpr int kGatherRegs = 16;      // logits gathered into registers: K <= 1024 in one round
 constexpr int kLeafCap = 2048;       // sparse leaf policy: legal ids per leaf (bk_mcts_leaf_logits)
-#ifndef BK_LEAF_BLOCKS
-#define BK_LEAF_BLOCKS 4
-#endif
-constexpr int kLeafBlocks = BK_LEAF_BLOCKS;  // workgroups per tree in k_leaf_logits
+constexpr int kLeafBlocks = 4;  // workgroups per tree in k_leaf_logits
 constexpr int kMaxFeat = 2048;       // policy-feature length staged in LDS
 constexpr int kLeafQ = 16;           // leaf logits: float4s of a W row a lane holds (F <= 1024)
 
@@ -63,21 +60,15 @@ struct DevMcts {
   int32_t* leaf_ids;    // [T*kLeafCap] sparse leaf policy: legal ids (ascending)
   float* leaf_logit;    // [T*kLeafCap] their logits
   int32_t* leaf_K;      // [T]
-  unsigned long long* counters;  // [8] (errors; the totals when BK_TREE_CTR is 0)
+  unsigned long long* counters;  // [8] (errors)
   unsigned long long* tree_ctr;  // [T*8] per-tree counters: uncontended atomics, summed on read
 };
 
-#ifndef BK_TREE_CTR
-#define BK_TREE_CTR 1  // A/B knob: per-tree counters (1) or one contended set for all trees (0)
-#endif
 // add v to counter k of tree t: fire-and-forget, on an address no other tree touches (every
 // tree on one shared counter serialised 256 atomics per stage in L2, which the workgroup's next
 // barrier then waited for)
 __device__ __forceinline__ void ctr_add(const struct DevMcts& m, int t, int k, unsigned long long v) {
-  if (BK_TREE_CTR)
-    atomicAdd(&m.tree_ctr[(size_t)t * 8 + k], v);
-  else
-    atomicAdd(&m.counters[k], v);
+  atomicAdd(&m.tree_ctr[(size_t)t * 8 + k], v);
 }
 
 enum { kCtrLevels = 2, kCtrExpanded = 3, kCtrTerminal = 4, kCtrErr = 5, kCtrScanned = 6, kCtrLeafK = 7 };
@@ -155,9 +146,7 @@ __device__ __forceinline__ void wave_argmax(double& best, int& bi) {
 // memory round trip: each lane loads all its children's (P, N, Q, id) first, the visit sum is
 // the wave's integer sum of N, then the lane scans its children in index order.
 constexpr int kSelB = 12;
-#ifndef BK_MASK_WPB
-#define BK_MASK_WPB 16  // A/B knob: waves that take orientations in a leaf bitmask (the rest idle)
-#endif
+constexpr int kMaskWpb = 16;  // waves that take orientations in a leaf bitmask (the rest idle)
 // eps: the term under the square root (mcts.py:43: 1e-6 with epsilon_fix, the default, else 0)
 __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, double cp, int& id_out,
                                             double eps = 1e-6) {
@@ -391,7 +380,7 @@ __device__ __forceinline__ void select_leaf(const DevPreset& dp, const DevMcts& 
     else if (NW == 1)
       build_mask_rows(dp, s, (int)s[kWToMove], m32);
     else
-      build_mask_rows_wg<(NW > BK_MASK_WPB ? BK_MASK_WPB : NW)>(dp, s, (int)s[kWToMove], m32, wave);
+      build_mask_rows_wg<(NW > kMaskWpb ? kMaskWpb : NW)>(dp, s, (int)s[kWToMove], m32, wave);
     BK_STAMP(0, 3);
     uint64_t* mo = m.leaf_mask + (size_t)t * dp.W64;
     uint64_t* mo2 = mask_out ? mask_out + (size_t)t * dp.W64 : nullptr;
@@ -1002,7 +991,7 @@ __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const
 }
 
 // The leaf bitmask of the state in LDS (s; m32 zeroed by the caller) built by whichever waves
-// call this: each claims slices k = 0..BK_MASK_WPB-1 (the orientations O % BK_MASK_WPB == k, the
+// call this: each claims slices k = 0..kMaskWpb-1 (the orientations O % kMaskWpb == k, the
 // slices of build_mask_rows_wg) from an LDS counter until none is left, ORing into m32. The
 // caller's barrier ends the build.
 __device__ __forceinline__ void mask_slices_claim(const DevPreset& dp, const uint32_t* s, uint32_t* m32, int* counter) {
@@ -1018,10 +1007,10 @@ __device__ __forceinline__ void mask_slices_claim(const DevPreset& dp, const uin
     int k = 0;
     if (lane_id() == 0) k = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     k = readlane_i(k, 0);
-    if (k >= BK_MASK_WPB) break;
+    if (k >= kMaskWpb) break;
     DevPreset dq = dp;  // the scalar sizes opaque per claim as well
     asm volatile("" : "+s"(dq.N), "+s"(dq.num_pieces));
-    orient_dispatch<BK_MASK_WPB>(dq, c, k, std::make_index_sequence<BK_MASK_WPB>{});
+    orient_dispatch<kMaskWpb>(dq, c, k, std::make_index_sequence<kMaskWpb>{});
   }
 }
 

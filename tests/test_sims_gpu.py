@@ -16,13 +16,16 @@ def _leaf_model(eng, blocks=2, seed=0):
     return LeafResNet(net, normalize=False, features=True).eval()
 
 
-@pytest.mark.parametrize("N,T,sims,overlap", [(20, 12, 9, "1"), (20, 12, 9, "0"), (14, 7, 6, "1"), (20, 64, 40, "1")])
-def test_leaf_step_matches_stagewise(N, T, sims, overlap, monkeypatch):
+@pytest.mark.parametrize("N,T,sims,overlap,skip0", [(20, 12, 9, "1", "1"), (20, 12, 9, "0", "1"), (14, 7, 6, "1", "1"),
+                                                    (20, 64, 40, "1", "1"), (20, 64, 40, "1", "0")])
+def test_leaf_step_matches_stagewise(N, T, sims, overlap, skip0, monkeypatch):
     """bk_mcts_leaf_step (policy head + expand/backup + the next descent in one launch; overlap 1
     = k_leaf_step_ov, the default, whose wave 0 backs up and descends while the other waves
     compute the logits) against k_leaf_logits -> k_expand_backup -> k_select: the same trees,
-    counters, leaf states and observations, bitwise."""
+    counters, leaf states and observations, bitwise — with the sparse head's zero-feature skip
+    (BK_LEAF_SKIP0=1, the default: W float4s of four zero features not loaded) and without it."""
     monkeypatch.setenv("BK_STEP_OVERLAP", overlap)
+    monkeypatch.setenv("BK_LEAF_SKIP0", skip0)
     from blokus_rl_amd.alphazero.batched_mcts import BatchedMCTS
     from blokus_rl_amd.boards import random_boards
     from blokus_rl_amd.engine import Engine

@@ -80,6 +80,59 @@ void run(const char* name, const h16x8* w, float* out, unsigned long long* clk) 
   printf("%-34s cycles per MFMA %.2f\n", name, (double)h[h.size() / 2] / (18.0 * 75));
 }
 
+
+// Two output blocks per wave (26 accumulators = 13 pixel groups x 2 blocks of 16 channels): one
+// B pair per group read from LDS feeds 6 products (the 2-blocks-per-wave form of k_leafnet_x3)
+template <int PF>
+__global__ __launch_bounds__(256, 1) void k2(const h16x8* __restrict__ w, float* out, unsigned long long* clk) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int l = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 2048; i += 256) reinterpret_cast<h16x8*>(lds)[i] = w[i];
+  h16x8 a[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) a[s] = w[s * 64 + l];
+  f32x4 acc[26];
+#pragma unroll
+  for (int g = 0; g < 26; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  auto addr = [&](int g) { return ((16 * g + (l & 15)) % 128) * 16 + (l >> 4) * 2048; };
+  h16x8 rb[8][2];
+#pragma unroll
+  for (int g = 0; g < PF; ++g) {
+    rb[g][0] = *reinterpret_cast<const h16x8*>(lds + addr(g));
+    rb[g][1] = *reinterpret_cast<const h16x8*>(lds + addr(g) + 8192);
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int rep = 0; rep < 18; ++rep) {
+#pragma unroll
+    for (int g = 0; g < 13; ++g) {
+      const int gp = g + PF;
+      rb[gp % 8][0] = *reinterpret_cast<const h16x8*>(lds + addr(gp));
+      rb[gp % 8][1] = *reinterpret_cast<const h16x8*>(lds + addr(gp) + 8192);
+      mfma3(acc[2 * g], a[0], a[1], rb[g % 8][0], rb[g % 8][1]);
+      mfma3(acc[2 * g + 1], a[2], a[3], rb[g % 8][0], rb[g % 8][1]);
+    }
+  }
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  float s = 0.f;
+#pragma unroll
+  for (int g = 0; g < 26; ++g) s += acc[g][0] + acc[g][1] + acc[g][2] + acc[g][3];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+  if (l == 0) clk[blockIdx.x * 4 + wave] = t1 - t0;
+}
+
+template <int PF>
+void run2(const char* name, const h16x8* w, float* out, unsigned long long* clk) {
+  const int blocks = 256;
+  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((k2<PF>), dim3(blocks), dim3(256), 32768, 0, w, out, clk);
+  hipDeviceSynchronize();
+  std::vector<unsigned long long> h(blocks * 4);
+  hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost);
+  std::sort(h.begin(), h.end());
+  printf("%-34s cycles per MFMA %.2f\n", name, (double)h[h.size() / 2] / (18.0 * 13 * 6));
+}
+
 int main() {
   h16x8* w;
   float* out;
@@ -102,6 +155,9 @@ int main() {
     run<1, 2>("  B from LDS, 2 triples ahead", w, out, clk);
     run<1, 4>("  B from LDS, 4 triples ahead", w, out, clk);
     run<1, 6>("  B from LDS, 6 triples ahead", w, out, clk);
+    run2<1>("  2 blocks/wave, B 1 group ahead", w, out, clk);
+    run2<2>("  2 blocks/wave, B 2 groups ahead", w, out, clk);
+    run2<3>("  2 blocks/wave, B 3 groups ahead", w, out, clk);
   }
   return 0;
 }
