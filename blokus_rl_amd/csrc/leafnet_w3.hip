@@ -54,6 +54,10 @@ __host__ __device__ constexpr int w3_write_unit(int g) {
 
 __device__ __forceinline__ int w3_swz(int C) { return ((C - 1) >> 1) & 7; }
 
+#ifndef BK_W3_ABL
+#define BK_W3_ABL 0  // timing ablations only (wrong outputs): 1 no V pieces, 2 no output transform, 4 no unit barriers
+#endif
+
 #if BK_LN_STAMP
 // timing diagnostics only (make w3stamps): per-wave s_memtime stamps of one launch, tools/w3/stamps_w3.py
 __device__ unsigned long long g_w3_stamps[256 * 4 * 128];
@@ -443,7 +447,9 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
         if (layer == 1) W3STAMP(4 + u);
         // the barrier: the V stores of this unit's slot done (all but the 8 grid reads of the
         // V after next, issued last, which may stay in flight across it)
-        if (u == 0 || u + 1 >= 4 * kW3Groups)
+        if (BK_W3_ABL & 4)
+          asm volatile("" ::: "memory");
+        else if (u == 0 || u + 1 >= 4 * kW3Groups)
           __syncthreads();
         else
           asm volatile("s_waitcnt lgkmcnt(8)\n\ts_barrier" ::: "memory");
@@ -475,7 +481,7 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
         constexpr int kSt = -1;
         const int su = (u == 9 ? 64 : (u == 12 ? 80 : (u == 10 ? 96 : kSt)));
         if (layer == 1 && su >= 0) W3STAMP(su);
-        if (more) {
+        if (more && !(BK_W3_ABL & 1)) {
           piece(0, (u + 1) & 3, dq, pr, slot ^ 1);
           piece(1, (u + 1) & 3, dq, pr, slot ^ 1);
         }
@@ -500,8 +506,8 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_w3(const float* __res
                 : "+v"(acc[p])
                 : "a"(U[p][1][0]), "v"(B[0]), "a"(U[p][1][1]), "v"(B[1]));
           if (layer == 1 && su >= 0) W3STAMP(su + 2 + i);  // after triple i
-          if (more && i + 2 < 8) piece(i + 2, (u + 1) & 3, dq, pr, slot ^ 1);
-          if (i >= 2 && i <= 4) {
+          if (more && i + 2 < 8 && !(BK_W3_ABL & 1)) piece(i + 2, (u + 1) & 3, dq, pr, slot ^ 1);
+          if (i >= 2 && i <= 4 && !(BK_W3_ABL & 2)) {
             if (xi > 0) zpart(i - 2, xi - 1, Yc);
             else if (g > 0) zpart(i - 2, 3, Yp);
           }

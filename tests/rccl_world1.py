@@ -59,18 +59,30 @@ def main():
     net_b.load_state_dict(net_a.state_dict())
     la = Learner(net_a, batch_size=64)
     out["ddp"] = type(la.net).__name__
-    loss_a = float(la.train_step(batch))
+    # Learner.train_step's work, split so the gradients can be read before the Adam step
+    la.net.train()
+    pa, va = la.net(batch["observation"])
+    loss_a = alphazero_loss(pa, va, batch, la.policy_fn)
+    la.optimizer.zero_grad(set_to_none=True)
+    loss_a.backward()
+    grads_a = [q.grad.detach().clone() for q in net_a.parameters()]
+    la.optimizer.step()
     opt = torch.optim.Adam(net_b.parameters(), lr=1e-3, weight_decay=1e-4)
     p, v = net_b(batch["observation"])
     loss_b = alphazero_loss(p, v, batch)
     opt.zero_grad(set_to_none=True)
     loss_b.backward()
+    grads_b = [q.grad.detach().clone() for q in net_b.parameters()]
     opt.step()
     torch.cuda.synchronize()
-    out["loss_ddp"], out["loss_plain"] = loss_a, float(loss_b)
+    out["loss_ddp"], out["loss_plain"] = float(loss_a), float(loss_b)
+    # gradients: the DDP all-reduce at world size 1 must leave them as the plain backward's, up to
+    # the run-to-run rounding of the training-mode conv backward (MIOpen)
+    out["grad_max_rel_diff"] = max(float((ga - gb).abs().max()) / (float(gb.abs().max()) + 1e-30)
+                                   for ga, gb in zip(grads_a, grads_b))
     diff = 0.0
-    for (n, pa), pb in zip(net_a.named_parameters(), net_b.parameters()):
-        diff = max(diff, float((pa.detach() - pb.detach()).abs().max()))
+    for (n, pa_), pb in zip(net_a.named_parameters(), net_b.parameters()):
+        diff = max(diff, float((pa_.detach() - pb.detach()).abs().max()))
     out["param_max_abs_diff"] = diff
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)

@@ -52,7 +52,10 @@ def test_rccl_world1_allgather_and_ddp():
     assert out["allgather_rows"] == 96 and out["allgather_equal"]
     assert out["ddp"] == "DistributedDataParallel"
     assert abs(out["loss_ddp"] - out["loss_plain"]) <= 1e-6 * max(1.0, abs(out["loss_plain"]))
-    assert out["param_max_abs_diff"] <= 1e-6
+    assert out["grad_max_rel_diff"] <= 1e-5
+    # one Adam step normalises each gradient element (lr g / (|g| + eps)): elements with |g| near
+    # eps = 1e-8 carry the backward's rounding into the step, so the parameters agree to ~1% of lr
+    assert out["param_max_abs_diff"] <= 1e-5
 
 
 def test_bench_selfplay_rccl_world1():
