@@ -223,6 +223,25 @@ def start_cpu_pool(n: int):
     return mp.get_context("spawn").Pool(n)
 
 
+def stop_cpu_pool(args) -> None:
+    """Join the CPU-baseline workers and end multiprocessing's resource tracker: the spawn pool's
+    semaphores register with that helper process, which otherwise outlives the bench (the driver
+    counted it as a leftover process, procs_at_end: 1). The pool must be unreferenced and collected
+    first so its semaphores unregister before the tracker stops."""
+    pool = getattr(args, "cpu_pool", None)
+    if pool is None:
+        return
+    pool.close()
+    pool.join()
+    args.cpu_pool = None
+    del pool
+    import gc
+    from multiprocessing import resource_tracker
+
+    gc.collect()
+    resource_tracker._resource_tracker._stop()
+
+
 def _pool_run(pool, fn, jobs):
     """Run jobs (one per worker) concurrently -> (sum of units, max seconds, per-worker units)."""
     res = pool.map(fn, jobs) if pool is not None else [fn(j) for j in jobs]
@@ -773,9 +792,8 @@ def main():
                 out["legal_move"]["cpu_baseline"] = cpu_baseline_legal(legal["_states"], args.cpu_seconds / 2, pool, nw)
                 out["ppo_vector_env"]["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2, pool, nw)
     out.pop("_states", None)
-    if args.cpu_pool is not None:
-        args.cpu_pool.close()
-        args.cpu_pool.join()
+    pool = largs = vargs = None  # (the Namespace copies hold the pool too)
+    stop_cpu_pool(args)
     if dist_active():
         out["dist_backend"] = dist.get_backend()
     if rank == 0:

@@ -352,6 +352,7 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
       return launch_check("k_legal_mask_staged");
     }
     case 11: BK_LEGAL_LAUNCH(1, 1); break;  // even/odd origin rows in separate LDS atomics: 15.1 vs 12.1 us
+    case 41: BK_LEGAL_LAUNCH(1, 2); break;  // lean orientation step (validity folded into the rows)
     default: BK_LEGAL_LAUNCH(1, 0); break;  // 1: one wave per group of 3 boards (the default)
   }
 #undef BK_LEGAL_LAUNCH

@@ -26,6 +26,7 @@ struct RowCtx {
   uint32_t upieces;    // wave-uniform: the pieces some board of the wave still has (skip the rest)
   int rN1;             // r * (N + 1): bit offset of origin row r is base + r*(N+1) - r*w
   int r;
+  int rw[6];           // lean form (SPLIT 2): rw[w] = r*(N+1) - r*w, opaque to the compiler
   uint32_t* mb;        // this lane's board bitmask in LDS
 };
 
@@ -55,6 +56,21 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
   for (int k = 1; k < oc.n; ++k) {
     bad |= c.fr[oc.dr[k]] << oc.dc[k];
     good |= c.ar[oc.dr[k]] << oc.dc[k];
+  }
+  if constexpr (SPLIT == 2) {
+    // lean form: the column and row validity live in fr (columns >= N and rows past the board
+    // forbidden, so a field bit past W or an origin row past N - h has a forbidden cell: every
+    // orientation has a cell at dc = 0 and one at dr = h - 1), and the field's bit offset is one
+    // add of the wave-uniform base to a per-lane constant: bitop3, brev, add, and, shift, shift, add
+    const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
+    const uint32_t v = __brev(good & ~bad & pmask);
+    const int bit = base + c.rw[oc.w];
+    const uint64_t x = (uint64_t)v << (bit & 31);
+    uint32_t* dst = c.mb + (bit >> 5);
+    atomicOr(dst, (uint32_t)x);
+    atomicOr(dst + 1, (uint32_t)(x >> 32));
+    base += R * W;
+    return;
   }
   const uint32_t colmask = (1u << W) - 1u;  // wave-uniform
   const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
@@ -328,14 +344,23 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   RowCtx c;
   c.fr[0] = __brev(forb);
   c.ar[0] = __brev(anch);
+  if constexpr (SPLIT == 2) c.fr[0] = ok ? __brev(forb | ~dp.full_row) : ~0u;
 #pragma unroll
   for (int d = 1; d < 5; ++d) {
     const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
     c.fr[d] = __shfl(c.fr[0], src, kWave);
     c.ar[d] = __shfl(c.ar[0], src, kWave);
+    if constexpr (SPLIT == 2) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
   }
   c.r = r;
   c.rN1 = r * (N + 1);
+  if constexpr (SPLIT == 2) {
+#pragma unroll
+    for (int w = 1; w < 6; ++w) {
+      c.rw[w] = c.rN1 - r * w;
+      asm volatile("" : "+v"(c.rw[w]));  // keep base + rw[w] one add (no re-association)
+    }
+  }
   c.pieces = pieces;
   // no piece skip here: with 3 boards per wave a piece absent from all three is rare, and the
   // branches cost the compiler its sharing of the shifted rows across orientations (+50% VALU)
@@ -344,7 +369,11 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32 + (j < bpw ? j : 0) * dp.W32pad;
   __syncthreads();  // mask zeroing complete
-  if constexpr (WPB > 1) {
+#ifndef BK_LEGAL_ABL
+#define BK_LEGAL_ABL 0  // diagnostic timing builds only: 1 no orientation work, 2 no mask stores
+#endif
+  if constexpr ((BK_LEGAL_ABL & 1) != 0) {
+  } else if constexpr (WPB > 1) {
     // each wave only its own orientations at compile-time bases: orient_all's walk over the
     // other waves' orientations (a scalar branch + base update each) doubled the instruction count
     orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
@@ -360,10 +389,30 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     if ((dp.W64 & 1) == 0) {
       const uint4* src = reinterpret_cast<const uint4*>(m32 + jj * dp.W32pad);
       uint4* dst = reinterpret_cast<uint4*>(masks + (size_t)(b0 + jj) * dp.W64);
-      for (int p = threadIdx.x; p < dp.W64 / 2; p += kWave * WPB) {
-        const uint4 v = src[p];
-        dst[p] = v;
-        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+      if constexpr ((BK_LEGAL_ABL & 4) != 0) {
+        // all of a board's LDS reads before its stores (4 x 64 uint4 cover W64 <= 512)
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int p = threadIdx.x + k * kWave * WPB;
+          v[k] = p < dp.W64 / 2 ? src[p] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int p = threadIdx.x + k * kWave * WPB;
+          if (p < dp.W64 / 2) dst[p] = v[k];
+          cnt += __popc(v[k].x) + __popc(v[k].y) + __popc(v[k].z) + __popc(v[k].w);
+        }
+      } else {
+        for (int p = threadIdx.x; p < dp.W64 / 2; p += kWave * WPB) {
+          const uint4 v = src[p];
+          if constexpr ((BK_LEGAL_ABL & 2) != 0) {
+            if (v.x == 0x9e3779b9u) dst[p] = v;  // (almost) never: the loads stay live
+          } else {
+            dst[p] = v;
+          }
+          cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        }
       }
     } else {
       for (int p = threadIdx.x; p < dp.W64; p += kWave * WPB) {

@@ -2,6 +2,8 @@
 different caps) with all_gather_packed; every rank must receive every row bit-exactly."""
 import os
 import socket
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -107,3 +109,18 @@ def test_bench_dry_world8_rows_intact():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["ranks_seen"] == list(range(8))
     assert out["rows_intact"] and out["value"] == sum(3 + r for r in range(8)) and out["common_cap"] == 128
+
+
+def test_bench_cpu_pool_leaves_no_process():
+    """bench.py's CPU-baseline pool ends with no child process left (the driver counted
+    multiprocessing's resource tracker as a leftover: procs_at_end 1 in BENCH_r04)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import argparse, psutil, bench\n"
+            "a = argparse.Namespace(cpu_pool=bench.start_cpu_pool(2))\n"
+            "assert a.cpu_pool.map(abs, [-1, 2]) == [1, 2]\n"
+            "bench.stop_cpu_pool(a)\n"
+            "print(len(psutil.Process().children(recursive=True)))\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "0"
+    assert "leaked" not in r.stderr and "Traceback" not in r.stderr, r.stderr[-2000:]

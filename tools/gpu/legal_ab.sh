@@ -1,13 +1,28 @@
 #!/bin/bash
-# config-2 legal kernel: tests, then this build vs BK_LIB=$1 interleaved (bench --workload legal)
+# k_legal_mask_rows: bit-exactness of the lean variant (BK_LEGAL_WPB=41) and of the diagnostic
+# store-order build, then per-launch times (tools/legal_scale.py) of the default, the lean variant
+# and the timing ablations (_lib/var/liblegal_abl<k>.so: 1 no orientation work, 2 no mask stores,
+# 4 LDS reads of a board before its stores, 5 = 1+4)
 cd "$GRAFT_REPO_ROOT" || exit 1
-out=gpurun_out/legal_ab
-mkdir -p $out
-timeout -k 10 300 python -u -m pytest tests/test_env_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $out/pytest.log 2>&1 || { tail -30 $out/pytest.log; exit 1; }
-tail -1 $out/pytest.log
-for i in 1 2 3; do
-  for lib in "" "$1"; do
-    BK_LIB=$lib timeout -k 10 120 python bench.py --workload legal --no-cpu-baseline > $out/l.json 2> $out/l.err || { tail -3 $out/l.err; exit 1; }
-    python -c "import json,sys; d=json.load(open('$out/l.json')); r=d['roofline']; print('lib [%s]' % sys.argv[1], round(d['value']/1e6,1), 'M boards/s', round(r['kernel_ms']*1e3,2), 'us frac', round(r['frac'],3))" "$lib"
-  done
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+out=gpurun_out/legal_ab.txt
+: > $out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_env_gpu.py \
+  -k "benchmark_boards or variants_bit_exact" >> $out 2>&1 || { echo "tests failed"; tail -20 $out; exit 1; }
+BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl4.so timeout -k 10 200 python -u -m pytest -x -q --timeout 120 \
+  --timeout-method thread tests/test_env_gpu.py -k "benchmark_boards" >> $out 2>&1 || { echo "abl4 tests failed"; tail -20 $out; exit 1; }
+run() {  # label, env...
+  local label=$1; shift
+  echo -n "$label " >> $out
+  env "$@" timeout -k 10 120 python tools/legal_scale.py 1024 4096 16384 >> $out 2>&1 || { echo "$label failed"; return 1; }
+}
+for rep in 1 2; do
+  run default BK_LEGAL_WPB=1 && run lean BK_LEGAL_WPB=41 \
+    && run abl1 BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl1.so \
+    && run abl2 BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl2.so \
+    && run abl4 BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl4.so \
+    && run abl5 BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl5.so \
+    && run abl4lean BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl4.so BK_LEGAL_WPB=41 || exit 1
 done
+grep -E "passed|failed|us_per_launch" $out
