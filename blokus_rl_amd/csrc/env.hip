@@ -328,6 +328,10 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
   const uint32_t* sp = (const uint32_t*)states;
 #define BK_LEGAL_LAUNCH(W, S) \
   hipLaunchKernelGGL((k_legal_mask_rows<W, S>), grid, dim3(64 * W), lds, st, c->dp, sp, players, B, mask_words, counts)
+#define BK_LEGAL_LAUNCH_NT(W, S)                                                                      \
+  hipLaunchKernelGGL((k_legal_mask_rows<W, S, 0, 20>), grid, dim3(64 * W), lds, st, c->dp, sp, players, B, \
+                     mask_words, counts)
+  const bool classic = c->dp.N == 20 && c->dp.num_pieces == kNumPieces;
   switch (c->legal_wpb) {
     case 2: BK_LEGAL_LAUNCH(2, 0); break;
     case 4: BK_LEGAL_LAUNCH(4, 0); break;
@@ -352,10 +356,17 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
       return launch_check("k_legal_mask_staged");
     }
     case 11: BK_LEGAL_LAUNCH(1, 1); break;  // even/odd origin rows in separate LDS atomics: 15.1 vs 12.1 us
-    case 41: BK_LEGAL_LAUNCH(1, 2); break;  // lean orientation step (validity folded into the rows)
+    // lean orientation step (validity folded into the rows), 41 on bit-reversed rows, 42 on rows
+    // in board order (no bit reversal), both at the compile-time board size when it is the classic
+    // board; 43 = 42 at the run-time size, 44 = the default step at the compile-time size
+    case 41: if (classic) BK_LEGAL_LAUNCH_NT(1, 2); else BK_LEGAL_LAUNCH(1, 2); break;
+    case 42: if (classic) BK_LEGAL_LAUNCH_NT(1, 3); else BK_LEGAL_LAUNCH(1, 3); break;
+    case 43: BK_LEGAL_LAUNCH(1, 3); break;
+    case 44: if (classic) BK_LEGAL_LAUNCH_NT(1, 0); else BK_LEGAL_LAUNCH(1, 0); break;
     default: BK_LEGAL_LAUNCH(1, 0); break;  // 1: one wave per group of 3 boards (the default)
   }
 #undef BK_LEGAL_LAUNCH
+#undef BK_LEGAL_LAUNCH_NT
   return launch_check("k_legal_mask_rows");
 }
 

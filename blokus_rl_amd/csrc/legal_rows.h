@@ -38,15 +38,39 @@ struct RowCtx {
 // otherwise the idle lanes and the empty rows, which all address the word of row 0, serialise on
 // it (the leaf bitmask of the search: 52.7 vs 53.8 us a leaf step). The 3-board legal kernel
 // keeps the unconditional form (its branch-free ORs measured 12.1 vs 15.4 us with the skip).
-template <int O, int WPB, int SPLIT, bool SKIP0 = false>
+// NT: the board size at compile time (20: the classic board with all 21 pieces), 0 = dp.N at run
+// time; with NT the piece test, W, R and the field bases are constants and the 91 steps are one
+// basic block (at run time every step is a scalar branch around an out-of-line block)
+template <int O, int WPB, int SPLIT, bool SKIP0 = false, int NT = 0>
 __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c, int wave, int& base) {
   constexpr OrientC oc = kOrient[O];
-  if (oc.piece >= dp.num_pieces) return;  // wave-uniform (presets use a prefix of the pieces)
-  const int W = dp.N - oc.w + 1;
-  const int R = dp.N - oc.h + 1;
+  if (NT ? oc.piece >= kNumPieces : oc.piece >= dp.num_pieces) return;  // wave-uniform (presets use a prefix of the pieces)
+  const int W = (NT ? NT : dp.N) - oc.w + 1;
+  const int R = (NT ? NT : dp.N) - oc.h + 1;
   // another wave of the workgroup owns this orientation, or no board of the wave has its piece
   // (scalar test; the bits stay as zeroed)
   if ((WPB > 1 && (O % WPB) != wave) || !((c.upieces >> oc.piece) & 1u)) {
+    base += R * W;
+    return;
+  }
+  if constexpr (SPLIT == 3) {
+    // the lean form on rows in board order (not bit-reversed): cell (dr, dc) of origin column c
+    // is bit c of row[dr] >> dc, so the field needs no v_bfrev (the shifts no longer fuse with
+    // their ORs: v_lshl_or has no right-shift twin)
+    uint32_t bad = c.fr[oc.dr[0]] >> oc.dc[0];
+    uint32_t good = c.ar[oc.dr[0]] >> oc.dc[0];
+#pragma unroll
+    for (int k = 1; k < oc.n; ++k) {
+      bad |= c.fr[oc.dr[k]] >> oc.dc[k];
+      good |= c.ar[oc.dr[k]] >> oc.dc[k];
+    }
+    const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
+    const uint32_t v = good & ~bad & pmask;
+    const int bit = base + c.rw[oc.w];
+    const uint64_t x = (uint64_t)v << (bit & 31);
+    uint32_t* dst = c.mb + (bit >> 5);
+    atomicOr(dst, (uint32_t)x);
+    atomicOr(dst + 1, (uint32_t)(x >> 32));
     base += R * W;
     return;
   }
@@ -101,11 +125,11 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
   base += R * W;
 }
 
-template <int WPB, int SPLIT, bool SKIP0 = false, size_t... Os>
+template <int WPB, int SPLIT, bool SKIP0 = false, int NT = 0, size_t... Os>
 __device__ __forceinline__ void orient_all(const DevPreset& dp, const RowCtx& c, int wave,
                                            std::index_sequence<Os...>) {
   int base = 0;
-  (orient_step<(int)Os, WPB, SPLIT, SKIP0>(dp, c, wave, base), ...);
+  (orient_step<(int)Os, WPB, SPLIT, SKIP0, NT>(dp, c, wave, base), ...);
 }
 
 // The bit offset of orientation O's fields in the mask, base(O) = sum over O' < O of
@@ -285,7 +309,7 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
 // orientations O with O % WPB == w (round robin keeps the cell work balanced), all OR into the
 // same LDS masks, then the WPB waves stream the masks out together.
 // LDS: boards_per_wave * W32pad words. Grid: ceil(B / boards_per_wave) blocks of 64*WPB.
-template <int WPB, int SPLIT, int BPW = 0>
+template <int WPB, int SPLIT, int BPW = 0, int NT = 0>
 __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, const uint32_t* __restrict__ states,
                                                               const int32_t* __restrict__ players, int B,
                                                               uint64_t* __restrict__ masks,
@@ -294,7 +318,7 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   __shared__ int cnt_sh[kWave];
   const int l = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int N = dp.N;
+  const int N = NT ? NT : dp.N;
   const int bpw = BPW ? BPW : kWave / N;
   const int j = l / N;
   const int r = l - j * N;
@@ -345,16 +369,20 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   c.fr[0] = __brev(forb);
   c.ar[0] = __brev(anch);
   if constexpr (SPLIT == 2) c.fr[0] = ok ? __brev(forb | ~dp.full_row) : ~0u;
+  if constexpr (SPLIT == 3) {
+    c.fr[0] = ok ? (forb | ~dp.full_row) : ~0u;
+    c.ar[0] = anch;
+  }
 #pragma unroll
   for (int d = 1; d < 5; ++d) {
     const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
     c.fr[d] = __shfl(c.fr[0], src, kWave);
     c.ar[d] = __shfl(c.ar[0], src, kWave);
-    if constexpr (SPLIT == 2) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
+    if constexpr (SPLIT >= 2) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
   }
   c.r = r;
   c.rN1 = r * (N + 1);
-  if constexpr (SPLIT == 2) {
+  if constexpr (SPLIT >= 2) {
 #pragma unroll
     for (int w = 1; w < 6; ++w) {
       c.rw[w] = c.rN1 - r * w;
@@ -378,7 +406,7 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     // other waves' orientations (a scalar branch + base update each) doubled the instruction count
     orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
   } else {
-    orient_all<WPB, SPLIT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
+    orient_all<WPB, SPLIT, false, NT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
   }
   __syncthreads();
   // stream out every board of the group: 16-B stores when rows are 16-B aligned (W64 even);
