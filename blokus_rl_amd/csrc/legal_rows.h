@@ -17,6 +17,10 @@
 namespace bk {
 
 __device__ const int kNoPlayer = -1;  // k_legal_mask_rows: the player read when none is given
+#ifndef BK_LEAN_ROWS
+#define BK_LEAN_ROWS 1  // A/B builds only: 0 = the single-board bitmasks on bit-reversed rows
+#endif
+constexpr bool kLeanRows = BK_LEAN_ROWS != 0;
 
 struct RowCtx {
   uint32_t fr[5];      // bit-reversed forbidden rows r..r+4
@@ -69,8 +73,15 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
     const int bit = base + c.rw[oc.w];
     const uint64_t x = (uint64_t)v << (bit & 31);
     uint32_t* dst = c.mb + (bit >> 5);
-    atomicOr(dst, (uint32_t)x);
-    atomicOr(dst + 1, (uint32_t)(x >> 32));
+    if (SKIP0) {
+      if (v) {
+        atomicOr(dst, (uint32_t)x);
+        if ((uint32_t)(x >> 32)) atomicOr(dst + 1, (uint32_t)(x >> 32));
+      }
+    } else {
+      atomicOr(dst, (uint32_t)x);
+      atomicOr(dst + 1, (uint32_t)(x >> 32));
+    }
     base += R * W;
     return;
   }
@@ -158,7 +169,7 @@ __device__ __forceinline__ void orient_step_at(const DevPreset& dp, const RowCtx
   if (oc.piece >= dp.num_pieces) return;  // wave-uniform
   const int N = dp.N;
   int base = kOrientBase.cnt[O] * N * N + kOrientBase.b[O] * N + kOrientBase.c[O];
-  orient_step<O, 1, 0, true>(dp, c, 0, base);
+  orient_step<O, 1, kLeanRows ? 3 : 0, true>(dp, c, 0, base);
 }
 template <int W, int WPB, size_t... Ks>
 __device__ __forceinline__ void orient_part(const DevPreset& dp, const RowCtx& c, std::index_sequence<Ks...>) {
@@ -174,7 +185,9 @@ __device__ __forceinline__ void orient_dispatch(const DevPreset& dp, const RowCt
 }
 
 // The row context of colour q on the board s (LDS) for lanes 0..N-1 (the board's rows); lanes
-// past N and rows past the board are masked by rowok. first: q has no cell yet.
+// past N and rows past the board are masked by rowok, or (kLeanRows: the single-board bitmasks of
+// the search use the lean step on board-order rows, as k_legal_mask_rows' variant 43) forbidden
+// outright in fr. first: q has no cell yet.
 __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32) {
   const int l = lane_id();
   const int N = dp.N;
@@ -194,16 +207,29 @@ __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
   RowCtx c;
-  c.fr[0] = __brev(forb);
-  c.ar[0] = __brev(anch);
+  if constexpr (kLeanRows) {
+    c.fr[0] = ok ? (forb | ~dp.full_row) : ~0u;
+    c.ar[0] = anch;
+  } else {
+    c.fr[0] = __brev(forb);
+    c.ar[0] = __brev(anch);
+  }
 #pragma unroll
   for (int d = 1; d < 5; ++d) {
     const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
     c.fr[d] = __shfl(c.fr[0], src, kWave);
     c.ar[d] = __shfl(c.ar[0], src, kWave);
+    if constexpr (kLeanRows) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
   }
   c.r = r;
   c.rN1 = r * (N + 1);
+  if constexpr (kLeanRows) {
+#pragma unroll
+    for (int w = 1; w < 6; ++w) {
+      c.rw[w] = c.rN1 - r * w;
+      asm volatile("" : "+v"(c.rw[w]));  // keep base + rw[w] one add
+    }
+  }
   c.pieces = s[kWPieces + q];
   c.upieces = __builtin_amdgcn_readfirstlane(c.pieces);
 #pragma unroll
@@ -222,6 +248,17 @@ __device__ __forceinline__ bool orient_any(const DevPreset& dp, const RowCtx& c,
     constexpr int O = decltype(oi)::value;
     constexpr OrientC oc = kOrient[O];
     if (found || oc.piece >= dp.num_pieces || !((c.upieces >> oc.piece) & 1u)) return;  // wave-uniform
+    if constexpr (kLeanRows) {
+      uint32_t bad = c.fr[oc.dr[0]] >> oc.dc[0];
+      uint32_t good = c.ar[oc.dr[0]] >> oc.dc[0];
+#pragma unroll
+      for (int k = 1; k < oc.n; ++k) {
+        bad |= c.fr[oc.dr[k]] >> oc.dc[k];
+        good |= c.ar[oc.dr[k]] >> oc.dc[k];
+      }
+      found = __ballot((good & ~bad) != 0u) != 0ull;
+      return;
+    }
     uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
     uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
 #pragma unroll
@@ -267,41 +304,10 @@ __device__ __forceinline__ void build_mask_rows_wg(const DevPreset& dp, const ui
 // item loop wherever a single wave owns a single board (k_select's leaf, k_legal_ids, ...).
 __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32) {
   const int l = lane_id();
-  const int N = dp.N;
   for (int i = l; i < dp.W32pad / 4; i += kWave) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
-  const bool ok = l < N;
-  const int r = ok ? l : 0;
-  const uint32_t own = ok ? s[q * kMaxN + r] : 0u;
-  const uint32_t occ = ok ? (s[r] | s[kMaxN + r] | s[2 * kMaxN + r] | s[3 * kMaxN + r]) : 0u;
-  const uint32_t up = (ok && r > 0) ? s[q * kMaxN + r - 1] : 0u;
-  const uint32_t dn = (ok && r + 1 < N) ? s[q * kMaxN + r + 1] : 0u;
-  const bool first = __ballot(own != 0u) == 0ull;
-  uint32_t forb = 0u, anch = 0u;
-  if (ok) {
-    forb = (occ | own << 1 | own >> 1 | up | dn) & dp.full_row;
-    if (first)
-      anch = (r == dp.corner_r(q)) ? (1u << dp.corner_c(q)) : 0u;
-    else
-      anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
-  }
-  RowCtx c;
-  c.fr[0] = __brev(forb);
-  c.ar[0] = __brev(anch);
-#pragma unroll
-  for (int d = 1; d < 5; ++d) {
-    const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
-    c.fr[d] = __shfl(c.fr[0], src, kWave);
-    c.ar[d] = __shfl(c.ar[0], src, kWave);
-  }
-  c.r = r;
-  c.rN1 = r * (N + 1);
-  c.pieces = s[kWPieces + q];
-  c.upieces = __builtin_amdgcn_readfirstlane(c.pieces);
-#pragma unroll
-  for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
-  c.mb = m32;
+  const RowCtx c = row_ctx(dp, s, q, m32);
   BK_BOARD_SYNC();
-  orient_all<1, 0, true>(dp, c, 0, std::make_index_sequence<kNumOrient>{});
+  orient_all<1, kLeanRows ? 3 : 0, true>(dp, c, 0, std::make_index_sequence<kNumOrient>{});
   BK_BOARD_SYNC();
 }
 
