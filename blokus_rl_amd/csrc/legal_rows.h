@@ -163,24 +163,26 @@ constexpr OrientBase kOrientBase = make_orient_base();
 // Wave W of WPB's orientations (O = W, W + WPB, ...) straight: no steps over the other waves'
 // orientations (stepping over 85 of 91 unrolled orientations per wave, each a scalar branch and
 // the base update, took ~14k cycles per leaf bitmask at 16 waves: the walk, not the work)
-template <int O>
+// LEAN: the context's rows are the lean board-order ones (row_ctx with kLeanRows), else bit-reversed
+template <int O, bool LEAN>
 __device__ __forceinline__ void orient_step_at(const DevPreset& dp, const RowCtx& c) {
   constexpr OrientC oc = kOrient[O];
   if (oc.piece >= dp.num_pieces) return;  // wave-uniform
   const int N = dp.N;
   int base = kOrientBase.cnt[O] * N * N + kOrientBase.b[O] * N + kOrientBase.c[O];
-  orient_step<O, 1, kLeanRows ? 3 : 0, true>(dp, c, 0, base);
+  orient_step<O, 1, LEAN ? 3 : 0, true>(dp, c, 0, base);
 }
-template <int W, int WPB, size_t... Ks>
+template <int W, int WPB, bool LEAN, size_t... Ks>
 __device__ __forceinline__ void orient_part(const DevPreset& dp, const RowCtx& c, std::index_sequence<Ks...>) {
-  (orient_step_at<W + (int)Ks * WPB>(dp, c), ...);
+  (orient_step_at<W + (int)Ks * WPB, LEAN>(dp, c), ...);
 }
-template <int WPB, size_t... Ws>
+template <int WPB, bool LEAN = kLeanRows, size_t... Ws>
 __device__ __forceinline__ void orient_dispatch(const DevPreset& dp, const RowCtx& c, int wave,
                                                 std::index_sequence<Ws...>) {
   // wave-uniform: each wave runs only its own instance
-  ((wave == (int)Ws ? orient_part<(int)Ws, WPB>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
-                    : void()),
+  ((wave == (int)Ws
+        ? orient_part<(int)Ws, WPB, LEAN>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
+        : void()),
    ...);
 }
 
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   } else if constexpr (WPB > 1) {
     // each wave only its own orientations at compile-time bases: orient_all's walk over the
     // other waves' orientations (a scalar branch + base update each) doubled the instruction count
-    orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
+    orient_dispatch<WPB, false>(dp, c, wave, std::make_index_sequence<WPB>{});
   } else {
     orient_all<WPB, SPLIT, false, NT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
   }
