@@ -356,14 +356,14 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
       return launch_check("k_legal_mask_staged");
     }
     case 11: BK_LEGAL_LAUNCH(1, 1); break;  // even/odd origin rows in separate LDS atomics: 15.1 vs 12.1 us
-    // lean orientation step (validity folded into the rows), 41 on bit-reversed rows, 42 on rows
-    // in board order (no bit reversal), both at the compile-time board size when it is the classic
-    // board; 43 = 42 at the run-time size, 44 = the default step at the compile-time size
-    case 41: if (classic) BK_LEGAL_LAUNCH_NT(1, 2); else BK_LEGAL_LAUNCH(1, 2); break;
-    case 42: if (classic) BK_LEGAL_LAUNCH_NT(1, 3); else BK_LEGAL_LAUNCH(1, 3); break;
-    case 43: BK_LEGAL_LAUNCH(1, 3); break;
-    case 44: if (classic) BK_LEGAL_LAUNCH_NT(1, 0); else BK_LEGAL_LAUNCH(1, 0); break;
-    default: BK_LEGAL_LAUNCH(1, 0); break;  // 1: one wave per group of 3 boards (the default)
+    case 40: BK_LEGAL_LAUNCH(1, 0); break;  // the round-4 step: bit-reversed rows, row/column masks
+    // lean steps on 2 / 3 waves per group (each wave every 2nd / 3rd orientation)
+    case 45: if (classic) BK_LEGAL_LAUNCH_NT(3, 3); else BK_LEGAL_LAUNCH(1, 3); break;
+    case 46: if (classic) BK_LEGAL_LAUNCH_NT(2, 3); else BK_LEGAL_LAUNCH(1, 3); break;
+    default:  // 1: one wave per group of 3 boards, the lean step (validity folded into the rows, which
+              // are in board order), at the compile-time size on the classic board
+      if (classic) BK_LEGAL_LAUNCH_NT(1, 3); else BK_LEGAL_LAUNCH(1, 3);
+      break;
   }
 #undef BK_LEGAL_LAUNCH
 #undef BK_LEGAL_LAUNCH_NT

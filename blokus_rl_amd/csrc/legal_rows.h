@@ -30,7 +30,7 @@ struct RowCtx {
   uint32_t upieces;    // wave-uniform: the pieces some board of the wave still has (skip the rest)
   int rN1;             // r * (N + 1): bit offset of origin row r is base + r*(N+1) - r*w
   int r;
-  int rw[6];           // lean form (SPLIT 2): rw[w] = r*(N+1) - r*w, opaque to the compiler
+  int rw[6];           // lean step (SPLIT 3): rw[w] = r*(N+1) - r*w, opaque to the compiler
   uint32_t* mb;        // this lane's board bitmask in LDS
 };
 
@@ -58,9 +58,13 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
     return;
   }
   if constexpr (SPLIT == 3) {
-    // the lean form on rows in board order (not bit-reversed): cell (dr, dc) of origin column c
-    // is bit c of row[dr] >> dc, so the field needs no v_bfrev (the shifts no longer fuse with
-    // their ORs: v_lshl_or has no right-shift twin)
+    // the lean step (the default of k_legal_mask_rows and, with kLeanRows, of the search's
+    // single-board bitmasks): rows in board order, so cell (dr, dc) of origin column c is bit c of
+    // row[dr] >> dc and the field needs no v_bfrev; the column and row validity live in fr
+    // (columns >= N and rows past the board forbidden: a field bit past W or an origin row past
+    // N - h then has a forbidden cell, since every orientation has a cell at dc = 0 and one at
+    // dr = h - 1); the field's bit offset is one add of the wave-uniform base to a per-lane
+    // constant. tests/test_legal_lean_algebra.py restates this arithmetic against the oracle.
     uint32_t bad = c.fr[oc.dr[0]] >> oc.dc[0];
     uint32_t good = c.ar[oc.dr[0]] >> oc.dc[0];
 #pragma unroll
@@ -91,21 +95,6 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
   for (int k = 1; k < oc.n; ++k) {
     bad |= c.fr[oc.dr[k]] << oc.dc[k];
     good |= c.ar[oc.dr[k]] << oc.dc[k];
-  }
-  if constexpr (SPLIT == 2) {
-    // lean form: the column and row validity live in fr (columns >= N and rows past the board
-    // forbidden, so a field bit past W or an origin row past N - h has a forbidden cell: every
-    // orientation has a cell at dc = 0 and one at dr = h - 1), and the field's bit offset is one
-    // add of the wave-uniform base to a per-lane constant: bitop3, brev, add, and, shift, shift, add
-    const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
-    const uint32_t v = __brev(good & ~bad & pmask);
-    const int bit = base + c.rw[oc.w];
-    const uint64_t x = (uint64_t)v << (bit & 31);
-    uint32_t* dst = c.mb + (bit >> 5);
-    atomicOr(dst, (uint32_t)x);
-    atomicOr(dst + 1, (uint32_t)(x >> 32));
-    base += R * W;
-    return;
   }
   const uint32_t colmask = (1u << W) - 1u;  // wave-uniform
   const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
@@ -182,6 +171,26 @@ __device__ __forceinline__ void orient_dispatch(const DevPreset& dp, const RowCt
   // wave-uniform: each wave runs only its own instance
   ((wave == (int)Ws
         ? orient_part<(int)Ws, WPB, LEAN>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
+        : void()),
+   ...);
+}
+
+// The lean step of orientation O at its compile-time base (board size NT): wave W of WPB runs the
+// orientations O = W, W + WPB, ... (k_legal_mask_rows' multi-wave lean variants)
+template <int O, int NT>
+__device__ __forceinline__ void orient_step_nt(const DevPreset& dp, const RowCtx& c) {
+  int base = kOrientBase.cnt[O] * NT * NT + kOrientBase.b[O] * NT + kOrientBase.c[O];
+  orient_step<O, 1, 3, false, NT>(dp, c, 0, base);
+}
+template <int W, int WPB, int NT, size_t... Ks>
+__device__ __forceinline__ void orient_part_nt(const DevPreset& dp, const RowCtx& c, std::index_sequence<Ks...>) {
+  (orient_step_nt<W + (int)Ks * WPB, NT>(dp, c), ...);
+}
+template <int WPB, int NT, size_t... Ws>
+__device__ __forceinline__ void orient_dispatch_nt(const DevPreset& dp, const RowCtx& c, int wave,
+                                                   std::index_sequence<Ws...>) {
+  ((wave == (int)Ws
+        ? orient_part_nt<(int)Ws, WPB, NT>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
         : void()),
    ...);
 }
@@ -317,6 +326,7 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
 // orientations O with O % WPB == w (round robin keeps the cell work balanced), all OR into the
 // same LDS masks, then the WPB waves stream the masks out together.
 // LDS: boards_per_wave * W32pad words. Grid: ceil(B / boards_per_wave) blocks of 64*WPB.
+constexpr int kLegalStoreIt = 4;  // uint4 rows per thread of the store phase: W64 / 2 <= 4 x 64 (N <= 20)
 template <int WPB, int SPLIT, int BPW = 0, int NT = 0>
 __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, const uint32_t* __restrict__ states,
                                                               const int32_t* __restrict__ players, int B,
@@ -376,7 +386,6 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   RowCtx c;
   c.fr[0] = __brev(forb);
   c.ar[0] = __brev(anch);
-  if constexpr (SPLIT == 2) c.fr[0] = ok ? __brev(forb | ~dp.full_row) : ~0u;
   if constexpr (SPLIT == 3) {
     c.fr[0] = ok ? (forb | ~dp.full_row) : ~0u;
     c.ar[0] = anch;
@@ -386,11 +395,11 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
     c.fr[d] = __shfl(c.fr[0], src, kWave);
     c.ar[d] = __shfl(c.ar[0], src, kWave);
-    if constexpr (SPLIT >= 2) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
+    if constexpr (SPLIT == 3) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
   }
   c.r = r;
   c.rN1 = r * (N + 1);
-  if constexpr (SPLIT >= 2) {
+  if constexpr (SPLIT == 3) {
 #pragma unroll
     for (int w = 1; w < 6; ++w) {
       c.rw[w] = c.rN1 - r * w;
@@ -409,6 +418,8 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
 #define BK_LEGAL_ABL 0  // diagnostic timing builds only: 1 no orientation work, 2 no mask stores
 #endif
   if constexpr ((BK_LEGAL_ABL & 1) != 0) {
+  } else if constexpr (WPB > 1 && SPLIT == 3 && NT > 0) {
+    orient_dispatch_nt<WPB, NT>(dp, c, wave, std::make_index_sequence<WPB>{});
   } else if constexpr (WPB > 1) {
     // each wave only its own orientations at compile-time bases: orient_all's walk over the
     // other waves' orientations (a scalar branch + base update each) doubled the instruction count
@@ -425,30 +436,23 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     if ((dp.W64 & 1) == 0) {
       const uint4* src = reinterpret_cast<const uint4*>(m32 + jj * dp.W32pad);
       uint4* dst = reinterpret_cast<uint4*>(masks + (size_t)(b0 + jj) * dp.W64);
-      if constexpr ((BK_LEGAL_ABL & 4) != 0) {
-        // all of a board's LDS reads before its stores (4 x 64 uint4 cover W64 <= 512)
-        uint4 v[4];
+      // all of the board's LDS reads before its stores (4 x 64 uint4 cover W64 <= 512 at N <= 20:
+      // the read-store round trip per 16 B cost ~0.5 us a launch at 4096 boards)
+      uint4 v[kLegalStoreIt];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int p = threadIdx.x + k * kWave * WPB;
-          v[k] = p < dp.W64 / 2 ? src[p] : make_uint4(0u, 0u, 0u, 0u);
-        }
+      for (int k = 0; k < kLegalStoreIt; ++k) {
+        const int p = threadIdx.x + k * kWave * WPB;
+        v[k] = p < dp.W64 / 2 ? src[p] : make_uint4(0u, 0u, 0u, 0u);
+      }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int p = threadIdx.x + k * kWave * WPB;
+      for (int k = 0; k < kLegalStoreIt; ++k) {
+        const int p = threadIdx.x + k * kWave * WPB;
+        if constexpr ((BK_LEGAL_ABL & 2) != 0) {
+          if (p < dp.W64 / 2 && v[k].x == 0x9e3779b9u) dst[p] = v[k];  // (almost) never: loads stay live
+        } else {
           if (p < dp.W64 / 2) dst[p] = v[k];
-          cnt += __popc(v[k].x) + __popc(v[k].y) + __popc(v[k].z) + __popc(v[k].w);
         }
-      } else {
-        for (int p = threadIdx.x; p < dp.W64 / 2; p += kWave * WPB) {
-          const uint4 v = src[p];
-          if constexpr ((BK_LEGAL_ABL & 2) != 0) {
-            if (v.x == 0x9e3779b9u) dst[p] = v;  // (almost) never: the loads stay live
-          } else {
-            dst[p] = v;
-          }
-          cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-        }
+        cnt += __popc(v[k].x) + __popc(v[k].y) + __popc(v[k].z) + __popc(v[k].w);
       }
     } else {
       for (int p = threadIdx.x; p < dp.W64; p += kWave * WPB) {

@@ -161,12 +161,14 @@ def test_hash_is_board_only(engines, oracles):
         assert int(st[b, 336:344].view(np.uint64)[0]) == o.hash(st[b])
 
 
-@pytest.mark.parametrize("wpb", ["2", "4", "8", "11", "14", "21", "31", "41", "42", "43", "44", "items"])
+@pytest.mark.parametrize("wpb", ["2", "4", "8", "11", "14", "21", "31", "40", "45", "46", "items"])
 def test_legal_kernel_variants_bit_exact(oracles, monkeypatch, wpb):
     """Every k_legal_mask_rows variant (BK_LEGAL_WPB: waves per board group, each wave only its own
     orientations; 11/14 = even and odd origin rows in separate LDS atomics; 21 = two boards per
-    wave; 31 = the staged kernel without LDS atomics; 41-44 = the lean orientation steps) and the
-    item-loop kernel give the oracle's masks on the config-2 boards and on 7x7 mid-game boards."""
+    wave; 31 = the staged kernel without LDS atomics; 40 = round 4's default step on bit-reversed
+    rows; 45 / 46 = the lean step on 3 / 2 waves per group; the default, the lean step on one wave,
+    is every other test's) and the item-loop kernel give the oracle's masks on the config-2 boards
+    and on 7x7 mid-game boards."""
     from blokus_rl_amd.boards import random_boards
     from blokus_rl_amd.engine import Engine
     if wpb == "items":

@@ -1,6 +1,6 @@
-"""Host check of the lean legal-mask step's algebra (legal_rows.h, orient_step SPLIT 2 / 3: the
-BK_LEGAL_WPB=41/42 kernels) against the oracle, before any GPU run: the lane arithmetic of one
-origin row — forbidden rows with the columns >= N and the rows past the board set (no column or
+"""Host check of the lean legal-mask step's algebra (legal_rows.h, orient_step SPLIT 3: the default
+k_legal_mask_rows, its multi-wave variants and the search's single-board bitmasks) against the
+oracle, before any GPU run: the lane arithmetic of one origin row — forbidden rows with the columns >= N and the rows past the board set (no column or
 row masks), the field's bit offset as base + rw[w], the 64-bit shift split over two words — is
 restated in 32-bit Python integers and must give the oracle's masks bit for bit
 (blokus_wrapper.py:108-132 via the oracle, oracle/oracle.py)."""
@@ -28,17 +28,13 @@ def _orient_table():
     return out
 
 
-def _brev(x: int) -> int:
-    return int(f"{x & M32:032b}"[::-1], 2)
-
-
 def _corners(N: int, P: int):
     if P == 4:
         return [(0, 0), (0, N - 1), (N - 1, 0), (N - 1, N - 1)]
     return [(0, 0), (N - 1, N - 1)]
 
 
-def _lean_mask(st: np.ndarray, N: int, P: int, num_pieces: int, reversed_rows: bool, rng) -> np.ndarray:
+def _lean_mask(st: np.ndarray, N: int, P: int, num_pieces: int, rng) -> np.ndarray:
     words = st.view(np.uint32)
     q = int(words[86])
     full = (1 << N) - 1
@@ -68,25 +64,19 @@ def _lean_mask(st: np.ndarray, N: int, P: int, num_pieces: int, reversed_rows: b
                 f, a = forb[r + d] | (~full & M32), anch[r + d]
             else:
                 f, a = M32, int(rng.integers(0, 1 << 32))
-            fr.append(_brev(f) if reversed_rows else f)
-            ar.append(_brev(a) if reversed_rows else a)
+            fr.append(f)
+            ar.append(a)
         rN1 = r * (N + 1)
         base = 0
         for p, h, w, dr, dc in table:
             if p >= num_pieces:
                 continue
             bad = good = 0
-            for a, b in zip(dr, dc):
-                if reversed_rows:
-                    bad |= (fr[a] << b) & M32
-                    good |= (ar[a] << b) & M32
-                else:
-                    bad |= fr[a] >> b
-                    good |= ar[a] >> b
+            for a, b in zip(dr, dc):  # cell (dr, dc) of origin column c: bit c of row[dr] >> dc
+                bad |= fr[a] >> b
+                good |= ar[a] >> b
             pm = M32 if (pieces >> p) & 1 else 0
             v = good & ~bad & pm & M32
-            if reversed_rows:
-                v = _brev(v)
             bit = base + rN1 - r * w
             x = v << (bit & 31)
             m32[bit >> 5] |= x & M32
@@ -95,15 +85,14 @@ def _lean_mask(st: np.ndarray, N: int, P: int, num_pieces: int, reversed_rows: b
     return np.array(m32, dtype=np.uint64)
 
 
-@pytest.mark.parametrize("reversed_rows", [True, False], ids=["41", "42"])
 @pytest.mark.parametrize("preset,nboards", [((20, 4, 5), 6), ((7, 2, 5), 8), ((7, 2, 4), 8)])
-def test_lean_step_algebra_matches_oracle(preset, nboards, reversed_rows):
+def test_lean_step_algebra_matches_oracle(preset, nboards):
     o = Oracle(*preset)
     rng = np.random.default_rng(11)
     for k in range(nboards):
         st = o.random_board(seed=100 + k, max_plies=6 * preset[1] + 4 * k)
         mask, _ = o.legal_mask(st)
         ref32 = mask.view(np.uint32).astype(np.uint64)
-        got = _lean_mask(st, preset[0], preset[1], o.num_pieces, reversed_rows, rng)
+        got = _lean_mask(st, preset[0], preset[1], o.num_pieces, rng)
         assert (got[: len(ref32)] == ref32).all(), (preset, k)
         assert not got[len(ref32):].any()
