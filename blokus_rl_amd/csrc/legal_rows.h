@@ -2,8 +2,10 @@
 //
 // Mapping: one 64-lane wave holds floor(64/N) boards, one lane per board row (N=20 -> 3 boards,
 // lanes 0-59; N=7 -> 9 boards). Each lane keeps its row and the next four rows of the mover's
-// forbidden / anchor bitboards BIT-REVERSED in registers, so "cell (dr, dc) of a placement with
-// origin column c" is bit (31-c) of rev_row[dr] << dc: one v_lshl_or_b32 per cell and plane.
+// forbidden / anchor bitboards in registers; in the batched kernel's default (lean) step in board
+// order, "cell (dr, dc) of a placement with origin column c" being bit c of row[dr] >> dc, and in
+// the search's single-board bitmasks BIT-REVERSED, bit (31-c) of rev_row[dr] << dc (one
+// v_lshl_or_b32 per cell and plane).
 // The 91 fixed orientations are unrolled at compile time from orient_table.h, so the inner
 // loop has no table loads and every cell offset is an immediate. For each orientation the lane
 // produces the W legal origin columns of its origin row and ORs that W-bit field into its
@@ -17,10 +19,6 @@
 namespace bk {
 
 __device__ const int kNoPlayer = -1;  // k_legal_mask_rows: the player read when none is given
-#ifndef BK_LEAN_ROWS
-#define BK_LEAN_ROWS 1  // A/B builds only: 0 = the single-board bitmasks on bit-reversed rows
-#endif
-constexpr bool kLeanRows = BK_LEAN_ROWS != 0;
 
 struct RowCtx {
   uint32_t fr[5];      // bit-reversed forbidden rows r..r+4
@@ -58,9 +56,8 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
     return;
   }
   if constexpr (SPLIT == 3) {
-    // the lean step (the default of k_legal_mask_rows and, with kLeanRows, of the search's
-    // single-board bitmasks): rows in board order, so cell (dr, dc) of origin column c is bit c of
-    // row[dr] >> dc and the field needs no v_bfrev; the column and row validity live in fr
+    // the lean step (k_legal_mask_rows' default): rows in board order, so cell (dr, dc) of origin
+    // column c is bit c of row[dr] >> dc and the field needs no v_bfrev; the column and row validity live in fr
     // (columns >= N and rows past the board forbidden: a field bit past W or an origin row past
     // N - h then has a forbidden cell, since every orientation has a cell at dc = 0 and one at
     // dr = h - 1); the field's bit offset is one add of the wave-uniform base to a per-lane
@@ -77,15 +74,8 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
     const int bit = base + c.rw[oc.w];
     const uint64_t x = (uint64_t)v << (bit & 31);
     uint32_t* dst = c.mb + (bit >> 5);
-    if (SKIP0) {
-      if (v) {
-        atomicOr(dst, (uint32_t)x);
-        if ((uint32_t)(x >> 32)) atomicOr(dst + 1, (uint32_t)(x >> 32));
-      }
-    } else {
-      atomicOr(dst, (uint32_t)x);
-      atomicOr(dst + 1, (uint32_t)(x >> 32));
-    }
+    atomicOr(dst, (uint32_t)x);
+    atomicOr(dst + 1, (uint32_t)(x >> 32));
     base += R * W;
     return;
   }
@@ -152,26 +142,24 @@ constexpr OrientBase kOrientBase = make_orient_base();
 // Wave W of WPB's orientations (O = W, W + WPB, ...) straight: no steps over the other waves'
 // orientations (stepping over 85 of 91 unrolled orientations per wave, each a scalar branch and
 // the base update, took ~14k cycles per leaf bitmask at 16 waves: the walk, not the work)
-// LEAN: the context's rows are the lean board-order ones (row_ctx with kLeanRows), else bit-reversed
-template <int O, bool LEAN>
+template <int O>
 __device__ __forceinline__ void orient_step_at(const DevPreset& dp, const RowCtx& c) {
   constexpr OrientC oc = kOrient[O];
   if (oc.piece >= dp.num_pieces) return;  // wave-uniform
   const int N = dp.N;
   int base = kOrientBase.cnt[O] * N * N + kOrientBase.b[O] * N + kOrientBase.c[O];
-  orient_step<O, 1, LEAN ? 3 : 0, true>(dp, c, 0, base);
+  orient_step<O, 1, 0, true>(dp, c, 0, base);
 }
-template <int W, int WPB, bool LEAN, size_t... Ks>
+template <int W, int WPB, size_t... Ks>
 __device__ __forceinline__ void orient_part(const DevPreset& dp, const RowCtx& c, std::index_sequence<Ks...>) {
-  (orient_step_at<W + (int)Ks * WPB, LEAN>(dp, c), ...);
+  (orient_step_at<W + (int)Ks * WPB>(dp, c), ...);
 }
-template <int WPB, bool LEAN = kLeanRows, size_t... Ws>
+template <int WPB, size_t... Ws>
 __device__ __forceinline__ void orient_dispatch(const DevPreset& dp, const RowCtx& c, int wave,
                                                 std::index_sequence<Ws...>) {
   // wave-uniform: each wave runs only its own instance
-  ((wave == (int)Ws
-        ? orient_part<(int)Ws, WPB, LEAN>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
-        : void()),
+  ((wave == (int)Ws ? orient_part<(int)Ws, WPB>(dp, c, std::make_index_sequence<(kNumOrient - (int)Ws + WPB - 1) / WPB>{})
+                    : void()),
    ...);
 }
 
@@ -196,9 +184,9 @@ __device__ __forceinline__ void orient_dispatch_nt(const DevPreset& dp, const Ro
 }
 
 // The row context of colour q on the board s (LDS) for lanes 0..N-1 (the board's rows); lanes
-// past N and rows past the board are masked by rowok, or (kLeanRows: the single-board bitmasks of
-// the search use the lean step on board-order rows, as k_legal_mask_rows' variant 43) forbidden
-// outright in fr. first: q has no cell yet.
+// past N and rows past the board are masked by rowok. first: q has no cell yet. (The lean step on
+// board-order rows here measured 0.3% slower end to end: the search's bitmasks skip used pieces
+// and zero fields, so their VALU is not on the step's critical path.)
 __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32) {
   const int l = lane_id();
   const int N = dp.N;
@@ -218,29 +206,16 @@ __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
   RowCtx c;
-  if constexpr (kLeanRows) {
-    c.fr[0] = ok ? (forb | ~dp.full_row) : ~0u;
-    c.ar[0] = anch;
-  } else {
-    c.fr[0] = __brev(forb);
-    c.ar[0] = __brev(anch);
-  }
+  c.fr[0] = __brev(forb);
+  c.ar[0] = __brev(anch);
 #pragma unroll
   for (int d = 1; d < 5; ++d) {
     const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
     c.fr[d] = __shfl(c.fr[0], src, kWave);
     c.ar[d] = __shfl(c.ar[0], src, kWave);
-    if constexpr (kLeanRows) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
   }
   c.r = r;
   c.rN1 = r * (N + 1);
-  if constexpr (kLeanRows) {
-#pragma unroll
-    for (int w = 1; w < 6; ++w) {
-      c.rw[w] = c.rN1 - r * w;
-      asm volatile("" : "+v"(c.rw[w]));  // keep base + rw[w] one add
-    }
-  }
   c.pieces = s[kWPieces + q];
   c.upieces = __builtin_amdgcn_readfirstlane(c.pieces);
 #pragma unroll
@@ -259,17 +234,6 @@ __device__ __forceinline__ bool orient_any(const DevPreset& dp, const RowCtx& c,
     constexpr int O = decltype(oi)::value;
     constexpr OrientC oc = kOrient[O];
     if (found || oc.piece >= dp.num_pieces || !((c.upieces >> oc.piece) & 1u)) return;  // wave-uniform
-    if constexpr (kLeanRows) {
-      uint32_t bad = c.fr[oc.dr[0]] >> oc.dc[0];
-      uint32_t good = c.ar[oc.dr[0]] >> oc.dc[0];
-#pragma unroll
-      for (int k = 1; k < oc.n; ++k) {
-        bad |= c.fr[oc.dr[k]] >> oc.dc[k];
-        good |= c.ar[oc.dr[k]] >> oc.dc[k];
-      }
-      found = __ballot((good & ~bad) != 0u) != 0ull;
-      return;
-    }
     uint32_t bad = c.fr[oc.dr[0]] << oc.dc[0];
     uint32_t good = c.ar[oc.dr[0]] << oc.dc[0];
 #pragma unroll
@@ -318,7 +282,7 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
   for (int i = l; i < dp.W32pad / 4; i += kWave) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
   const RowCtx c = row_ctx(dp, s, q, m32);
   BK_BOARD_SYNC();
-  orient_all<1, kLeanRows ? 3 : 0, true>(dp, c, 0, std::make_index_sequence<kNumOrient>{});
+  orient_all<1, 0, true>(dp, c, 0, std::make_index_sequence<kNumOrient>{});
   BK_BOARD_SYNC();
 }
 
@@ -423,7 +387,7 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   } else if constexpr (WPB > 1) {
     // each wave only its own orientations at compile-time bases: orient_all's walk over the
     // other waves' orientations (a scalar branch + base update each) doubled the instruction count
-    orient_dispatch<WPB, false>(dp, c, wave, std::make_index_sequence<WPB>{});
+    orient_dispatch<WPB>(dp, c, wave, std::make_index_sequence<WPB>{});
   } else {
     orient_all<WPB, SPLIT, false, NT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
   }

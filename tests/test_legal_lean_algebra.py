@@ -1,6 +1,5 @@
 """Host check of the lean legal-mask step's algebra (legal_rows.h, orient_step SPLIT 3: the default
-k_legal_mask_rows, its multi-wave variants and the search's single-board bitmasks) against the
-oracle, before any GPU run: the lane arithmetic of one origin row — forbidden rows with the columns >= N and the rows past the board set (no column or
+k_legal_mask_rows and its multi-wave variants) against the oracle, before any GPU run: the lane arithmetic of one origin row — forbidden rows with the columns >= N and the rows past the board set (no column or
 row masks), the field's bit offset as base + rw[w], the 64-bit shift split over two words — is
 restated in 32-bit Python integers and must give the oracle's masks bit for bit
 (blokus_wrapper.py:108-132 via the oracle, oracle/oracle.py)."""
