@@ -100,6 +100,18 @@ __device__ __forceinline__ int wave_sum(int x) {
   BK_WAVE_SCAN(x, dpp_i, op_add_i);
   return readlane_i(x, kWave - 1);
 }
+// The wave total of x (integer add), uniform: a reduction into lane 63, not a scan — each DPP step
+// reads 0 where the scan masks a lane (bound_ctrl, and the rows a broadcast does not write keep the
+// `old` 0), so the adds need no lane selects (~12 VALU instead of the scan's ~24).
+__device__ __forceinline__ int wave_total(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8: lane 15 of a row = its sum
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1 and 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2 and 3
+  return readlane_i(x, kWave - 1);
+}
 __device__ __forceinline__ float wave_sum_f(float x) {
   BK_WAVE_SCAN(x, dpp_f, op_add_f);
   return readlane_f(x, kWave - 1);

@@ -331,7 +331,8 @@ int bk_legal_mask(bk_ctx* c, const void* states, const int32_t* players, int B, 
 #define BK_LEGAL_LAUNCH_NT(W, S)                                                                      \
   hipLaunchKernelGGL((k_legal_mask_rows<W, S, 0, 20>), grid, dim3(64 * W), lds, st, c->dp, sp, players, B, \
                      mask_words, counts)
-  const bool classic = c->dp.N == 20 && c->dp.num_pieces == kNumPieces;
+  const bool classic = c->dp.N == 20 && c->dp.num_pieces == kNumPieces && c->dp.W64 == kClassicW64 &&
+                       c->dp.W32pad == kClassicW32pad;
   switch (c->legal_wpb) {
     case 2: BK_LEGAL_LAUNCH(2, 0); break;
     case 4: BK_LEGAL_LAUNCH(4, 0); break;

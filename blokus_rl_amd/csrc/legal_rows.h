@@ -291,6 +291,7 @@ __device__ __forceinline__ void build_mask_rows(const DevPreset& dp, const uint3
 // same LDS masks, then the WPB waves stream the masks out together.
 // LDS: boards_per_wave * W32pad words. Grid: ceil(B / boards_per_wave) blocks of 64*WPB.
 constexpr int kLegalStoreIt = 4;  // uint4 rows per thread of the store phase: W64 / 2 <= 4 x 64 (N <= 20)
+constexpr int kClassicW64 = 476, kClassicW32pad = 952;  // the classic board's mask rows (30433 ids)
 template <int WPB, int SPLIT, int BPW = 0, int NT = 0>
 __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, const uint32_t* __restrict__ states,
                                                               const int32_t* __restrict__ players, int B,
@@ -298,6 +299,10 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
                                                               int32_t* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t m32[];
   __shared__ int cnt_sh[kWave];
+#ifndef BK_LEGAL_ABL
+#define BK_LEGAL_ABL 0  // diagnostic timing builds only: 1 no orientation work, 2 no mask stores, 8 empty
+#endif
+  if constexpr ((BK_LEGAL_ABL & 8) != 0) return;
   const int l = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int N = NT ? NT : dp.N;
@@ -307,9 +312,19 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   const int b0 = blockIdx.x * bpw;
   const int b = b0 + j;
   const bool ok = j < bpw && b < B;
-  for (int i = threadIdx.x; i < bpw * dp.W32pad / 4; i += kWave * WPB)
-    reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (threadIdx.x < kWave) cnt_sh[threadIdx.x] = 0;
+  if constexpr (NT > 0 && WPB == 1) {
+    // the classic board: 3 boards x 238 uint4 (W32pad = 952), a compile-time trip count
+    constexpr int kZ = (3 * kClassicW32pad / 4 + kWave - 1) / kWave;
+#pragma unroll
+    for (int k = 0; k < kZ; ++k) {
+      const int i = l + k * kWave;
+      if (k < kZ - 1 || i < 3 * kClassicW32pad / 4) reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  } else {
+    for (int i = threadIdx.x; i < bpw * dp.W32pad / 4; i += kWave * WPB)
+      reinterpret_cast<uint4*>(m32)[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x < kWave) cnt_sh[threadIdx.x] = 0;
+  }
 
   uint32_t o0 = 0u, o1 = 0u, o2 = 0u, o3 = 0u, pieces4[kMaxP] = {0u, 0u, 0u, 0u};
   int q = 0;
@@ -378,9 +393,6 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
   for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
   c.mb = m32 + (j < bpw ? j : 0) * dp.W32pad;
   __syncthreads();  // mask zeroing complete
-#ifndef BK_LEGAL_ABL
-#define BK_LEGAL_ABL 0  // diagnostic timing builds only: 1 no orientation work, 2 no mask stores
-#endif
   if constexpr ((BK_LEGAL_ABL & 1) != 0) {
   } else if constexpr (WPB > 1 && SPLIT == 3 && NT > 0) {
     orient_dispatch_nt<WPB, NT>(dp, c, wave, std::make_index_sequence<WPB>{});
@@ -392,6 +404,43 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     orient_all<WPB, SPLIT, false, NT>(dp, c, wave, std::make_index_sequence<kNumOrient>{});
   }
   __syncthreads();
+  if constexpr (NT > 0 && WPB == 1) {
+    // the classic board, one wave: all 3 x 4 LDS reads, then the 16-B stores; the counts of
+    // boards 0 and 1 share one wave reduction (16-bit halves: a count is < 2^15), stored by lane 0
+    constexpr int kRow4 = kClassicW64 / 2;  // uint4 per board mask
+    uint4 v[3][kLegalStoreIt];
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+      for (int k = 0; k < kLegalStoreIt; ++k) {
+        const int p = l + k * kWave;
+        v[jj][k] = (k < kLegalStoreIt - 1 || p < kRow4)
+                       ? reinterpret_cast<const uint4*>(m32 + jj * kClassicW32pad)[p]
+                       : make_uint4(0u, 0u, 0u, 0u);
+      }
+    int cnt[3] = {0, 0, 0};
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const bool live = b0 + jj < B;
+      uint4* dst = reinterpret_cast<uint4*>(masks + (size_t)(b0 + jj) * kClassicW64);
+#pragma unroll
+      for (int k = 0; k < kLegalStoreIt; ++k) {
+        const int p = l + k * kWave;
+        if (live && (k < kLegalStoreIt - 1 || p < kRow4)) {
+          if constexpr ((BK_LEGAL_ABL & 2) == 0) dst[p] = v[jj][k];
+        }
+        cnt[jj] += __popc(v[jj][k].x) + __popc(v[jj][k].y) + __popc(v[jj][k].z) + __popc(v[jj][k].w);
+      }
+    }
+    const int c01 = wave_total(cnt[0] | (cnt[1] << 16));
+    const int c2 = wave_total(cnt[2]);
+    if (counts && l == 0) {
+      counts[b0] = c01 & 0xFFFF;
+      if (b0 + 1 < B) counts[b0 + 1] = (int)((unsigned)c01 >> 16);
+      if (b0 + 2 < B) counts[b0 + 2] = c2;
+    }
+    return;
+  }
   // stream out every board of the group: 16-B stores when rows are 16-B aligned (W64 even);
   // popcounts accumulate per lane, one wave reduction and one LDS add per board
   const int nb = B - b0 < bpw ? B - b0 : bpw;

@@ -13,7 +13,9 @@ run() {  # label, env...
   echo "$label $(env "$@" timeout -k 10 120 python tools/legal_scale.py 1024 4096 16384 2>/dev/null)" >> $out
 }
 for rep in 1 2; do
-  run default BK_LEGAL_WPB=1 && run r4step BK_LEGAL_WPB=40 && run lean3w BK_LEGAL_WPB=45 \
-    && run lean2w BK_LEGAL_WPB=46 || exit 1
+  run default BK_LEGAL_WPB=1 && run r4step BK_LEGAL_WPB=40 \
+    && run abl1_no_orient BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl1.so \
+    && run abl2_no_stores BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl2.so \
+    && run abl8_empty BK_LIB=blokus_rl_amd/_lib/var/liblegal_abl8.so || exit 1
 done
 grep -E "passed|failed|us_per_launch" $out
