@@ -77,10 +77,13 @@ class BatchedMCTS:
                                             _ptr(weight), _ptr(bias), self._s()))
 
     def leaf_step(self, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, values: torch.Tensor,
-                  roots: torch.Tensor | None = None, active: torch.Tensor | None = None, cpuct: float = 1.0):
+                  roots: torch.Tensor | None = None, active: torch.Tensor | None = None, cpuct: float = 1.0,
+                  want_mask: bool = True):
         """leaf_logits(feat, weight, bias) + expand_backup(None, values, 2) and, when roots is given,
         the next select(roots, active, cpuct) in one launch (bk_mcts_leaf_step; the same trees
-        bitwise). Returns select's (status, obs, mask) or None."""
+        bitwise). Returns select's (status, obs, mask) or None. want_mask=False: the next leaves'
+        bitmasks are not copied out (the engine keeps its own for the next step; self-play's
+        captured graph reads only status and obs), and the returned mask is stale."""
         assert feat.dtype == torch.float32 and feat.shape[0] == self.T and feat.stride(1) == 1
         assert weight.is_contiguous() and weight.shape == (self.eng.A, feat.shape[1]) and bias.shape == (self.eng.A,)
         assert values.dtype == torch.float32 and values.shape == (self.T, self.eng.P)
@@ -88,7 +91,8 @@ class BatchedMCTS:
         _check(self.lib.bk_mcts_leaf_step(self.h, ctypes.c_void_p(feat.data_ptr()), feat.stride(0), feat.shape[1],
                                           _ptr(weight), _ptr(bias), _ptr(values), int(sel), _ptr(roots),
                                           _ptr(active), float(cpuct), _ptr(self.status) if sel else None,
-                                          _ptr(self.obs) if sel else None, _ptr(self.leaf_mask) if sel else None,
+                                          _ptr(self.obs) if sel else None,
+                                          _ptr(self.leaf_mask) if sel and want_mask else None,
                                           self._s()))
         return (self.status, self.obs, self.leaf_mask) if sel else None
 

@@ -307,7 +307,7 @@ class SelfPlay:
                         out, v = ev._forward(obs)
                         last = i == self.sim_graph_sims - 1
                         self.mcts.leaf_step(out, ev.policy_w, ev.policy_b, v, None if last else self._g_roots,
-                                            self._g_active, self.cpuct)
+                                            self._g_active, self.cpuct, want_mask=False)
                 else:
                     for _ in range(self.sim_graph_sims):
                         self._sim_body()

@@ -137,7 +137,8 @@ int bk_mcts_reset(bk_mcts* m, const int32_t* reset_flags, void* stream);
  * the table or a terminal board. Outputs per tree:
  *   leaf_status[t]: 0 inactive, 1 needs NN evaluation, 2 terminal (value = one-hot scores)
  *   obs[t]: the leaf observation [2P][N][N] f32 (written for status 1) — the NN input batch
- *   leaf_mask: [T][mask_words] legal bits of the leaf (status 1), for the masked softmax. */
+ *   leaf_mask: [T][mask_words] legal bits of the leaf (status 1), for the masked softmax; may be
+ *   null (the engine keeps its own copy for the expansion). */
 int bk_mcts_select(bk_mcts* m, const void* roots, const int32_t* active, double cpuct,
                    int32_t* leaf_status, float* obs, uint64_t* leaf_mask, void* stream);
 /* The same with the root's exploration term under the square root given: mcts.py:43 adds
