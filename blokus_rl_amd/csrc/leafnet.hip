@@ -315,7 +315,18 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
     ln_mfma_drain(acc);
     if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
     const bool last = layer + 1 == nlayers;
-    if (!last) {
+#ifndef BK_LN_ABL
+#define BK_LN_ABL 0  // timing diagnostics only (wrong outputs): 1 no grid writes or barriers between tower
+                     // convs, 2 = 1 without the epilogue arithmetic as well
+#endif
+    if (!last && BK_LN_ABL != 0) {
+      if constexpr ((BK_LN_ABL & 2) == 0) {
+        const int ex_out = scale_exp(bnd_a * max_in + bnd_b);
+        const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
+        max_in = fmaxf(max_in, mx);  // keep the arithmetic live
+        ex = ex_out;
+      }
+    } else if (!last) {
       const int ex_out = scale_exp(bnd_a * max_in + bnd_b);  // = out_exp(layer + 1, max_in)
       const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
       if (layer == 1) LNSTAMP(21, __builtin_amdgcn_s_memtime());
