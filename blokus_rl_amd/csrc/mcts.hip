@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #ifdef BK_STAMPS
   // diag: 0 start, 1 the new node's entry published (wave 1), 2 wave 0 backup done, 3 wave 0 descent done, 4 the last logit
-  // wave done, 5 its children stored, 6 the next leaf's bitmask done (all waves), 7 end, 8 wave 0 out of the
+  // wave done, 9 its children's stores issued, 5 its children stored, 6 the next leaf's bitmask done (all waves), 7 end, 8 wave 0 out of the
   // bitmask claims (select_leaf's own stamps: g_stamps[0][t][4] stores issued, [5] observation issued)
 #define BK_OV_STAMP(i) \
   do { if (lane_id() == 0 && do_select && t < 4096) g_step_stamps[t][i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -263,6 +263,7 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_leaf_step_ov(DevPreset dp, 
         __builtin_amdgcn_s_sleep(1);
       const int err = readlane_i(sx.err, 0);
       if (err == 0) expand_children_lds(m, (int64_t)sx.off, K, ids, lg);
+      BK_OV_STAMP(9);  // the children's stores issued
       // the flag orders the children before the descent's reads of them; once the descent is over
       // nobody reads them in this launch, so the stores drain under the bitmask instead of being
       // waited for here (the kernel's end orders them for the next launch)
@@ -388,6 +389,9 @@ extern "C" {
 #ifdef BK_STAMPS
 int bk_debug_stamps(unsigned long long* out) {  // [2][4096][8] host copy
   return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)), "stamps");
+}
+int bk_debug_mask_stamps(unsigned long long* out) {  // [256][16][6] host copy: leaf bitmask claims
+  return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mask_stamps), sizeof(g_mask_stamps)), "mask stamps");
 }
 int bk_debug_step_stamps(unsigned long long* out) {  // [4096][16] host copy: k_leaf_step phases
   return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamps), sizeof(g_step_stamps)), "step stamps");

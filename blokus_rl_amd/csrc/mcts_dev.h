@@ -994,9 +994,23 @@ __device__ __forceinline__ int leaf_logits_prologue_w(const DevPreset& dp, const
 // call this: each claims slices k = 0..kMaskWpb-1 (the orientations O % kMaskWpb == k, the
 // slices of build_mask_rows_wg) from an LDS counter until none is left, ORing into m32. The
 // caller's barrier ends the build.
+#ifdef BK_STAMPS
+// diag: per (tree, wave) of the leaf bitmask claims: entry, slices claimed, exit, longest slice, the
+// last slice run again with its code just executed (ORs the same bits), the first claim
+static __device__ unsigned long long g_mask_stamps[256][16][6];
+#endif
 __device__ __forceinline__ void mask_slices_claim(const DevPreset& dp, const uint32_t* s, uint32_t* m32, int* counter) {
+#ifdef BK_STAMPS
+  const unsigned long long t_in = __builtin_amdgcn_s_memtime();
+  unsigned long long n_cl = 0, t_max = 0, t_first_claim = 0;
+  int last_k = -1;
+#endif
   RowCtx c = row_ctx(dp, s, (int)s[kWToMove], m32);
   for (;;) {
+#ifdef BK_STAMPS
+    const unsigned long long t_s = __builtin_amdgcn_s_memtime();
+    if (t_first_claim == 0) t_first_claim = t_s;
+#endif
     // the context opaque per claim: nothing derived from it is hoisted out of the loop (the
     // compiler would otherwise keep every slice's shifted rows live at once)
 #pragma unroll
@@ -1011,7 +1025,33 @@ __device__ __forceinline__ void mask_slices_claim(const DevPreset& dp, const uin
     DevPreset dq = dp;  // the scalar sizes opaque per claim as well
     asm volatile("" : "+s"(dq.N), "+s"(dq.num_pieces));
     orient_dispatch<kMaskWpb>(dq, c, k, std::make_index_sequence<kMaskWpb>{});
+#ifdef BK_STAMPS
+    ++n_cl;
+    last_k = k;
+    const unsigned long long d = __builtin_amdgcn_s_memtime() - t_s;
+    t_max = d > t_max ? d : t_max;
+#endif
   }
+#ifdef BK_STAMPS
+  const unsigned long long t_out = __builtin_amdgcn_s_memtime();
+  unsigned long long t_warm = 0;
+  if (last_k >= 0) {
+    DevPreset dq = dp;
+    asm volatile("" : "+s"(dq.N), "+s"(dq.num_pieces));
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    orient_dispatch<kMaskWpb>(dq, c, last_k, std::make_index_sequence<kMaskWpb>{});
+    t_warm = __builtin_amdgcn_s_memtime() - t0;
+  }
+  const int w = (int)(threadIdx.x >> 6);
+  if (lane_id() == 0 && blockIdx.x < 256 && w < 16) {
+    g_mask_stamps[blockIdx.x][w][0] = t_in;
+    g_mask_stamps[blockIdx.x][w][1] = n_cl;
+    g_mask_stamps[blockIdx.x][w][2] = t_out;
+    g_mask_stamps[blockIdx.x][w][3] = t_max;
+    g_mask_stamps[blockIdx.x][w][4] = t_warm;
+    g_mask_stamps[blockIdx.x][w][5] = t_first_claim;
+  }
+#endif
 }
 
 // The new node's children from the logits in LDS (ids[i], lg[i], i < K), by one wave:

@@ -40,11 +40,25 @@ out = {"trees": int(ok.sum()), "total_median": float(np.median(rel[:, 7])), "tot
 for i, nm in zip([1, 2, 3, 4, 5, 6, 7], names):
     out[nm] = {"median": float(np.median(rel[:, i])), "p90": float(np.percentile(rel[:, i], 90)),
                "max": float(rel[:, i].max())}
-extra = {"wave0 out of mask claims": a[:, 8] - a[:, 0], "select_leaf stores issued": g0[:, 4] - a[:, 0],
+extra = {"children stores issued": a[:, 9] - a[:, 0], "wave0 out of mask claims": a[:, 8] - a[:, 0], "select_leaf stores issued": g0[:, 4] - a[:, 0],
          "select_leaf obs issued": g0[:, 5] - a[:, 0], "descent probe (sum)": g0[:, 6], "descent PUCT scan (sum)": g0[:, 7],
          "descent placement (sum)": g1[:, 7], "descent next-mover check (sum)": g1[:, 6]}
 for nm, v in extra.items():
     out[nm] = {"median": float(np.median(v)), "p90": float(np.percentile(v, 90)), "max": float(v.max())}
+# the leaf bitmask claims per (tree, wave): entry / exit relative to the tree's start, slices, longest slice
+lib.bk_debug_mask_stamps.argtypes = [ctypes.c_void_p]
+ms = np.zeros((256, 16, 6), dtype=np.uint64)
+if lib.bk_debug_mask_stamps(ms.ctypes.data_as(ctypes.c_void_p)) == 0:
+    ms = ms[ok].astype(np.int64)
+    t0 = a[:, :1]
+    ent, ex = ms[:, :, 0] - t0, ms[:, :, 2] - t0
+    out["mask claims"] = {"entry_median_per_wave": np.median(ent, axis=0).tolist(),
+                          "exit_median_per_wave": np.median(ex, axis=0).tolist(),
+                          "slices_mean_per_wave": ms[:, :, 1].mean(axis=0).round(2).tolist(),
+                          "longest_slice_median": float(np.median(ms[:, :, 3].max(axis=1))),
+                          "slice_median_of_claiming_waves": float(np.median(ms[:, :, 3][ms[:, :, 1] > 0])),
+                          "warm_slice_median": float(np.median(ms[:, :, 4][ms[:, :, 1] > 0])),
+                          "row_ctx_median": float(np.median((ms[:, :, 5] - ms[:, :, 0])[ms[:, :, 1] > 0]))}
 slow = np.argsort(rel[:, 7])[-10:]
 out["slowest10"] = [[int(x) for x in rel[j, 1:]] for j in slow]
 K = sp.mcts.__dict__.get("_k", None)
