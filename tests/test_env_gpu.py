@@ -153,6 +153,23 @@ def test_benchmark_boards_bit_exact(engines, oracles):
     assert (_np(masks).view(np.uint64) == ref_masks).all()
 
 
+@pytest.mark.parametrize("B", [1, 2, 4, 5, 1022])
+def test_legal_mask_ragged_groups(engines, oracles, B):
+    """The classic board's lean kernel handles 3 boards per wave: batches that leave 1 or 2 boards
+    in the last group (and batches of one group or less) give the oracle's masks and counts, and
+    write nothing past the last board."""
+    from blokus_rl_amd.boards import random_boards
+    eng, o = engines[(20, 4, 5)], oracles[(20, 4, 5)]
+    st = random_boards(eng, B, seed0=11)
+    masks = torch.full((B + 1, eng.W), -1, dtype=torch.int64, device=eng.device)
+    counts = torch.full((B + 1,), -7, dtype=torch.int32, device=eng.device)
+    eng.legal_mask_into(st, masks[:B], counts[:B])
+    ref_masks, ref_counts = o.legal_mask_batch(_np(st))
+    assert (_np(counts[:B]) == ref_counts).all()
+    assert (_np(masks[:B]).view(np.uint64) == ref_masks).all()
+    assert int(counts[B]) == -7 and bool((masks[B] == -1).all())
+
+
 def test_hash_is_board_only(engines, oracles):
     eng, o = engines[(20, 4, 5)], oracles[(20, 4, 5)]
     from blokus_rl_amd.boards import random_boards
