@@ -611,30 +611,36 @@ def bench_train(args, world, rank):
 
     eng = Engine(20, 4, 5)
     res = {}
-    for bs in (args.train_batch, 64):
+    # the learner's default ("auto": the device path at large batches), the same batch on the
+    # fp32 MIOpen path, and the reference's batch 64
+    for key, bs, dpath in (("main", args.train_batch, "auto"), ("fp32", args.train_batch, False), ("b64", 64, "auto")):
         r = bench_learner(eng, world, rank, bs, args.train_steps, 3, rows=args.train_rows,
-                          reference_steps=0 if (args.no_cpu_baseline or bs != 64) else 10,
-                          barrier=(lambda: _barrier(world)))
+                          reference_steps=0 if (args.no_cpu_baseline or key != "b64") else 10,
+                          barrier=(lambda: _barrier(world)), device_path=dpath)
         dt = _max_over_ranks(r["elapsed_s"], world)
         r["value"] = bs * args.train_steps * world / dt
         r["unit"] = "samples/s"
         r["ms_per_step"] = dt / args.train_steps * 1e3
-        res[bs] = r
-    main_r = res[args.train_batch]
+        res[key] = r
+    main_r = res["main"]
     lk = main_r["loss_kernels"]
     out = {"metric": "AlphaZero learner samples/sec (20x20 ResNet-5x64, Adam, device replay batches)",
            "value": main_r["value"], "unit": "samples/s", "n_gpus": world, "steps": args.train_steps,
            "ms_per_step": main_r["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-           "dtype": "fp32", "data": "synthetic replay: random-play boards, Dirichlet pi, one-hot z",
+           "dtype": "fp32 (tower convs: split-f16 x3 products, fp32-class)" if main_r["device_path"] else "fp32", "data": "synthetic replay: random-play boards, Dirichlet pi, one-hot z",
            "config": {"workload": "§8f row 1 learner", "batch_per_gpu": args.train_batch,
                       "global_batch": args.train_batch * world, "parallelism": f"ddp{world}"},
-           "at_reference_batch_64": {k: res[64][k] for k in ("value", "unit", "ms_per_step")},
+           "device_path": main_r["device_path"],
+           "path": ("tower convs (forward + input gradient) on bk_conv_x3 (split-f16 MFMA, fp32-class), "
+                    "channels_last, PyTorch batch norm" if main_r["device_path"] else "fp32 MIOpen"),
+           "fp32_miopen_same_batch": {k: res["fp32"][k] for k in ("value", "unit", "ms_per_step")},
+           "at_reference_batch_64": {k: res["b64"][k] for k in ("value", "unit", "ms_per_step", "device_path")},
            "roofline": {"bound": "hbm", "kernel": lk["kernel"], "achieved": lk["achieved_GBps"],
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk["achieved_GBps"] * 1e9 / HBM_PEAK,
                         "kernel_ms": lk["ms"], "bytes_per_launch_pair": lk["bytes_per_launch_pair"],
                         "units_per_launch": args.train_batch, "traffic": None}}
-    if "reference_path" in res[64]:
-        out["reference_path_batch_64"] = res[64]["reference_path"]
+    if "reference_path" in res["b64"]:
+        out["reference_path_batch_64"] = res["b64"]["reference_path"]
     return out
 
 

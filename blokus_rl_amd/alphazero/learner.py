@@ -118,9 +118,20 @@ class Learner:
     """Adam on the reference's net with the device batch path; DDP when a process group is up."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 1e-3, weight_decay: float = 1e-4, batch_size: int = 64,
-                 seed: int = 0, policy_fn=policy_loss, group=None, optimizer: torch.optim.Optimizer | None = None):
+                 seed: int = 0, policy_fn=policy_loss, group=None, optimizer: torch.optim.Optimizer | None = None,
+                 device_path: bool | str = "auto"):
+        """device_path: train the ResNet on train_conv's device path (tower convs on bk_conv_x3,
+        channels_last, PyTorch batch norm; switched in place) — True, False, or "auto" = on a GPU
+        at batch_size >= 256 (the large batches where the fp32 convolutions dominate a step)."""
         self.model = model
         self.batch_size = batch_size
+        on_gpu = next(model.parameters()).is_cuda
+        if device_path == "auto":
+            device_path = on_gpu and batch_size >= 256
+        self.device_path = bool(device_path)
+        if self.device_path:
+            from .train_conv import prepare_model
+            prepare_model(model)
         self.policy_fn = policy_fn
         self.group = group
         up = dist.is_available() and dist.is_initialized()
@@ -138,7 +149,10 @@ class Learner:
     def train_step(self, batch: dict) -> torch.Tensor:
         """train_step (neural_network.py:52-85) without the host sync: returns the loss tensor."""
         self.net.train()
-        p_pred, v_pred = self.net(batch["observation"])
+        obs = batch["observation"]
+        if self.device_path:
+            obs = obs.contiguous(memory_format=torch.channels_last)
+        p_pred, v_pred = self.net(obs)
         loss = alphazero_loss(p_pred, v_pred, batch, self.policy_fn)
         self.optimizer.zero_grad(set_to_none=True)
         loss.backward()

@@ -123,13 +123,13 @@ def bench_reference_path(eng, states, ids, pi, k, z, batch: int, steps: int, mod
 
 
 def bench_learner(eng, world: int, rank: int, batch: int, steps: int, warmup: int, rows: int = 8192,
-                  reference_steps: int = 0, barrier=None):
+                  reference_steps: int = 0, barrier=None, device_path: bool | str = "auto"):
     buf, cap, states, ids, pi, k, z = synthetic_replay(eng, rows, seed=1000 * rank)
     rb = DeviceReplay(eng, cap=cap)
     rb.add_packed(buf, cap)
     torch.manual_seed(0)
     model = ResNet(eng.N, eng.P, eng.A, 5).to(eng.device)
-    L = Learner(model, lr=1e-3, weight_decay=1e-4, batch_size=batch, seed=rank)
+    L = Learner(model, lr=1e-3, weight_decay=1e-4, batch_size=batch, seed=rank, device_path=device_path)
     gen = torch.Generator(device=eng.device).manual_seed(rank)
     idx = [torch.randint(0, rows, (batch,), device=eng.device, generator=gen) for _ in range(steps + warmup)]
     for i in range(warmup):
@@ -153,7 +153,7 @@ def bench_learner(eng, world: int, rank: int, batch: int, steps: int, warmup: in
         lp, _ = model(b["observation"])
     kms = time_loss_kernels(lp.contiguous(), b["ids"], b["pi"], b["k"])
     kbytes = loss_kernel_bytes(b["k"])
-    out = {"batch_per_gpu": batch, "steps": steps, "elapsed_s": dt, "loss": float(loss),
+    out = {"batch_per_gpu": batch, "steps": steps, "elapsed_s": dt, "loss": float(loss), "device_path": L.device_path,
            "loss_kernels": {"kernel": "k_policy_loss + k_policy_loss_grad", "ms": kms,
                             "bytes_per_launch_pair": kbytes, "achieved_GBps": kbytes / (kms * 1e-3) / 1e9}}
     if reference_steps and rank == 0 and world == 1:

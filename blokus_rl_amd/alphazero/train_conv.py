@@ -1,0 +1,114 @@
+"""The learner's device path for the ResNet: the residual tower's 3x3
+convolutions 64 -> 64 on the f16 matrix cores (bk_conv_x3: split-f16 products, fp32-class), the
+activations in channels_last (NHWC) and batch norm on PyTorch's own kernels.
+
+The reference trains models/blokus_nnet.py:88-151 in fp32 (neural_network.py:52-85); on MI355X
+the fp32 convolutions (MIOpen igemm / Winograd on the f32 MFMA, 1/16 of the f16 rate on gfx950)
+take most of a large-batch step. `ConvX3Function` runs a conv's forward and its input gradient
+through bk_conv_x3 (the weight gradient stays on MIOpen's fp32 path); `prepare_model` switches a
+ResNet to that path in place without touching its parameters or state_dict keys.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from ..engine import _check, _ptr, _stream, load_library
+from ..nets import use_native_batchnorm
+
+
+def pack_weight(weight: torch.Tensor, flip: bool) -> tuple[torch.Tensor, torch.Tensor]:
+    """[64, 64, 3, 3] f32 -> (split fragments, inverse row scales) of bk_conv_x3, on the device
+    (bk_conv_x3_pack: nets.pack_x3's operands; flip = the input-gradient conv's weights)."""
+    lib = load_library()
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    ws = torch.empty(lib.bk_conv_x3_weight_bytes(), dtype=torch.uint8, device=w.device)
+    inv = torch.empty(64, dtype=torch.float32, device=w.device)
+    _check(lib.bk_conv_x3_pack(_ptr(w), int(flip), _ptr(ws), _ptr(inv), _stream(w.device)))
+    return ws, inv
+
+
+def conv_x3(x: torch.Tensor, ws: torch.Tensor, inv: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    """bk_conv_x3 on a channels_last [B, 64, 20, 20] f32 activation -> [B, 64, 20, 20] channels_last."""
+    lib = load_library()
+    B, C, N, N2 = x.shape
+    if C != 64 or N != 20 or N2 != 20 or x.dtype != torch.float32 or not x.is_cuda:
+        raise ValueError(f"conv_x3 takes a [B, 64, 20, 20] f32 device tensor, got {tuple(x.shape)} {x.dtype}")
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.empty((B, 64, N, N), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    b = None
+    if bias is not None:
+        b = bias.detach()
+        b = b if (b.dtype == torch.float32 and b.is_contiguous()) else b.float().contiguous()
+    # NHWC: channels_last [B, 64, N, N] is the dense [B][N][N][64] buffer the kernel reads and writes
+    _check(lib.bk_conv_x3(ctypes.c_void_p(x.data_ptr()), B, N, _ptr(ws), _ptr(inv), _ptr(b) if b is not None else None,
+                          ctypes.c_void_p(y.data_ptr()), _stream(x.device)))
+    return y
+
+
+class ConvX3Function(torch.autograd.Function):
+    """y = conv2d(x, weight, bias, padding=1) with the forward and the input gradient on
+    bk_conv_x3; the weight gradient on PyTorch's convolution backward (fp32), the bias gradient
+    the sum of dy over batch and pixels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ws, inv = pack_weight(weight, flip=False)
+        y = conv_x3(x, ws, inv, bias)
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            ws, inv = pack_weight(weight, flip=True)
+            gx = conv_x3(gy, ws, inv, None)
+        if ctx.needs_input_grad[1]:
+            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, stride=1, padding=1)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum(dim=(0, 2, 3))
+        return gx, gw, gb
+
+
+def _eligible(m: nn.Module) -> bool:
+    return (type(m) is nn.Conv2d and m.in_channels == 64 and m.out_channels == 64 and m.kernel_size == (3, 3)
+            and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1) and m.groups == 1
+            and m.padding_mode == "zeros")
+
+
+class X3Conv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters and state_dict keys) whose 20x20 64->64 device calls run
+    ConvX3Function; anything else (CPU, other shapes) takes nn.Conv2d's own path."""
+
+    def forward(self, x):
+        if x.is_cuda and x.dim() == 4 and tuple(x.shape[1:]) == (64, 20, 20) and x.dtype == torch.float32:
+            return ConvX3Function.apply(x, self.weight, self.bias)
+        return super().forward(x)
+
+
+def use_x3_convs(model: nn.Module) -> int:
+    """Switch every eligible Conv2d (3x3, 64 -> 64, stride 1, padding 1) to X3Conv2d in place;
+    returns how many were switched."""
+    k = 0
+    for m in model.modules():
+        if _eligible(m):
+            m.__class__ = X3Conv2d
+            k += 1
+    return k
+
+
+def prepare_model(model: nn.Module, x3_convs: bool = True) -> nn.Module:
+    """The device training path in place: channels_last parameters, PyTorch batch norm, and
+    (x3_convs) the tower convs on bk_conv_x3."""
+    use_native_batchnorm(model)
+    if x3_convs:
+        use_x3_convs(model)
+    return model.to(memory_format=torch.channels_last)

@@ -18,6 +18,27 @@ import torch.nn.functional as F
 from torch import nn
 
 
+class NativeBatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d on PyTorch's own batch-norm kernels instead of MIOpen's (same parameters,
+    buffers and state_dict keys; training-mode batch statistics and running-stat updates alike)."""
+
+    def forward(self, x):
+        prev = torch._C._get_cudnn_enabled()
+        torch._C._set_cudnn_enabled(False)  # F.batch_norm reads the flag; the backward follows the forward
+        try:
+            return super().forward(x)
+        finally:
+            torch._C._set_cudnn_enabled(prev)
+
+
+def use_native_batchnorm(model: nn.Module) -> nn.Module:
+    """Switch every BatchNorm2d of `model` to NativeBatchNorm2d in place."""
+    for m in model.modules():
+        if type(m) is nn.BatchNorm2d:
+            m.__class__ = NativeBatchNorm2d
+    return model
+
+
 class ResNet(nn.Module):
     def __init__(self, board_size: int, num_players: int, action_size: int, num_res_blocks: int = 5,
                  channels: int = 64):

@@ -265,6 +265,20 @@ int bk_policy_loss_grad(const float* x, int64_t ldx, const int16_t* ids, const f
                         int cap, int B, const float* lse, float scale, const float* gscale, float* grad,
                         int64_t ldg, void* stream);
 
+/* The learner's 3x3 convolutions 64 -> 64 (stride 1, zero padding 1; the residual tower of
+ * models/blokus_nnet.py:103-112 as neural_network.py:52-85 trains it) on split-f16 MFMA products
+ * with fp32-class accuracy (trainconv.hip: the leaf net's x3 arithmetic, one launch per conv):
+ * y[b][p][o] = sum_{tap, c} W[o][c][tap] x[b][p + tap][c] (+ bias[o]), x and y NHWC
+ * [B][N][N][64] f32, N = 20. The forward pass uses W = the layer's weight; the input gradient
+ * uses the same call on dy with W[o][c][tap] = weight[c][o][8 - tap] (bk_conv_x3_pack flip = 1).
+ * wsplit (bk_conv_x3_weight_bytes() bytes) and inv [64] come from bk_conv_x3_pack on the device
+ * (weight [64][64][3][3] f32, PyTorch's Conv2d layout). Replaces the fp32 convolution calls
+ * (MIOpen) of the training step; bias may be NULL. */
+int bk_conv_x3_weight_bytes(void);
+int bk_conv_x3_pack(const float* w, int flip, void* wsplit, float* inv, void* stream);
+int bk_conv_x3(const float* x, int B, int N, const void* wsplit, const float* inv, const float* bias, float* y,
+               void* stream);
+
 /* ---------------------------------------------------------------- PPO
  * PPOTrainer._compute_gae (ppo/trainer.py:177-211) + returns = advantages + values (:83) for a
  * rollout of T steps x E envs ([T][E] f32, row t = step t): float32, the reference's operation
