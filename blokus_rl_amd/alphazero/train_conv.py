@@ -5,7 +5,7 @@ activations in channels_last (NHWC) and batch norm on PyTorch's own kernels.
 The reference trains models/blokus_nnet.py:88-151 in fp32 (neural_network.py:52-85); on MI355X
 the fp32 convolutions (MIOpen igemm / Winograd on the f32 MFMA, 1/16 of the f16 rate on gfx950)
 take most of a large-batch step. `ConvX3Function` runs a conv's forward and its input gradient
-through bk_conv_x3 (the weight gradient stays on MIOpen's fp32 path); `prepare_model` switches a
+through bk_conv_x3 and its weight gradient through bk_conv_x3_wgrad; `prepare_model` switches a
 ResNet to that path in place without touching its parameters or state_dict keys.
 """
 from __future__ import annotations
@@ -50,10 +50,26 @@ def conv_x3(x: torch.Tensor, ws: torch.Tensor, inv: torch.Tensor, bias: torch.Te
     return y
 
 
+def conv_x3_wgrad(x: torch.Tensor, gy: torch.Tensor) -> torch.Tensor:
+    """bk_conv_x3_wgrad: the weight gradient [64, 64, 3, 3] of the 20x20 64->64 conv from its
+    input x and output gradient gy (channels_last [B, 64, 20, 20] f32)."""
+    lib = load_library()
+    B = x.shape[0]
+    x = x.contiguous(memory_format=torch.channels_last)
+    gy = gy.contiguous(memory_format=torch.channels_last)
+    if tuple(x.shape[1:]) != (64, 20, 20) or x.shape != gy.shape or x.dtype != torch.float32 or gy.dtype != torch.float32:
+        raise ValueError("conv_x3_wgrad takes two [B, 64, 20, 20] f32 tensors")
+    ws = torch.empty(lib.bk_conv_x3_wgrad_workspace_floats(B), dtype=torch.float32, device=x.device)
+    dw = torch.empty((64, 64, 3, 3), dtype=torch.float32, device=x.device)
+    _check(lib.bk_conv_x3_wgrad(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(gy.data_ptr()), B, 20, _ptr(ws), _ptr(dw),
+                                _stream(x.device)))
+    return dw
+
+
 class ConvX3Function(torch.autograd.Function):
-    """y = conv2d(x, weight, bias, padding=1) with the forward and the input gradient on
-    bk_conv_x3; the weight gradient on PyTorch's convolution backward (fp32), the bias gradient
-    the sum of dy over batch and pixels."""
+    """y = conv2d(x, weight, bias, padding=1) with the forward, the input gradient and the weight
+    gradient on bk_conv_x3 / bk_conv_x3_wgrad; the bias gradient the sum of dy over batch and
+    pixels."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -72,7 +88,7 @@ class ConvX3Function(torch.autograd.Function):
             ws, inv = pack_weight(weight, flip=True)
             gx = conv_x3(gy, ws, inv, None)
         if ctx.needs_input_grad[1]:
-            gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, stride=1, padding=1)
+            gw = conv_x3_wgrad(x, gy)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum(dim=(0, 2, 3))
         return gx, gw, gb

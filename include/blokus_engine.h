@@ -275,6 +275,13 @@ int bk_policy_loss_grad(const float* x, int64_t ldx, const int16_t* ids, const f
  * (weight [64][64][3][3] f32, PyTorch's Conv2d layout). Replaces the fp32 convolution calls
  * (MIOpen) of the training step; bias may be NULL. */
 int bk_conv_x3_weight_bytes(void);
+/* The weight gradient of the same conv on split-f16 MFMA products: dw[o][c][ky][kx] (PyTorch's
+ * layout, f32) = sum over b and pixels p of dy[b][p][o] * x[b][p + (ky - 1, kx - 1)][c] (zero
+ * padding); x, dy NHWC [B][N][N][64] f32, N = 20; workspace: bk_conv_x3_wgrad_workspace_floats(B)
+ * floats (per-workgroup partial sums, added in a fixed order: deterministic). Replaces the
+ * fp32 weight-gradient convolution (MIOpen) of the training step. */
+int bk_conv_x3_wgrad_workspace_floats(int B);
+int bk_conv_x3_wgrad(const float* x, const float* dy, int B, int N, float* workspace, float* dw, void* stream);
 int bk_conv_x3_pack(const float* w, int flip, void* wsplit, float* inv, void* stream);
 int bk_conv_x3(const float* x, int B, int N, const void* wsplit, const float* inv, const float* bias, float* y,
                void* stream);
