@@ -4,8 +4,9 @@
 // training step's forward (y = conv(x) + b) and its input gradient (dx = conv(dy, w flipped and
 // transposed)) leave the fp32 MFMA / MIOpen path for the f16 matrix cores at fp32-class accuracy.
 //
-// One workgroup per board (4 waves, wave w = output channels 16w..16w+15), as k_leafnet_x3's
-// tower layer: the board's NHWC input comes from HBM, is scaled by a power of two so that its
+// One workgroup per CU walking boards b = blockIdx.x, += gridDim.x (4 waves, wave w = output
+// channels 16w..16w+15), each board as k_leafnet_x3's tower layer: the next board's NHWC input is
+// loaded into registers under the current board's MFMAs; a board's input is scaled by a power of two so that its
 // largest magnitude lies in [2^14, 2^15) (the board maximum: a block reduction), split into f16
 // halves and written into the zero-haloed LDS planes of leafnet_common.h; the 18 K-chunks (9 taps
 // x 2 halves of 32 input channels) then run the same ring-fed MFMA loop (ln_chunk), and the
@@ -22,7 +23,7 @@ namespace {
 template <int N>
 __global__ __launch_bounds__(kLnThreads, 1) void k_conv_x3(const float* __restrict__ x, const h16x8* __restrict__ w,
                                                            const float* __restrict__ inv,
-                                                           const float* __restrict__ bias, float* __restrict__ y) {
+                                                           const float* __restrict__ bias, float* __restrict__ y, int B) {
   constexpr int NN = N * N, RS = ln_row(N), NG = ln_groups(N), PL = ln_plane(N);
   constexpr int QN = NN * 16, QIT = (QN + kLnThreads - 1) / kLnThreads;  // float4 quads of the board
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -31,17 +32,20 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_conv_x3(const float* __restri
   const int tid = threadIdx.x, l = tid & 63, n = l & 15, ks = l >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int oc = 16 * wave + 4 * ks;
-  const size_t b = blockIdx.x;
 
-  // the board's input first (its HBM latency under the halo zeroing and the weight loads)
-  const f32x4* xb = reinterpret_cast<const f32x4*>(x + b * NN * 64);
+  // a board's input into registers (issued one board ahead: its HBM latency under the MFMAs)
   f32x4 xv[QIT];
+  auto load = [&](int b) {
+    const f32x4* xb = reinterpret_cast<const f32x4*>(x + (size_t)b * NN * 64);
 #pragma unroll
-  for (int i = 0; i < QIT; ++i) {
-    const int q = tid + i * kLnThreads;
-    xv[i] = q < QN ? __builtin_nontemporal_load(xb + q) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  {  // zero the halo of the 16 planes (k_leafnet_x3's map)
+    for (int i = 0; i < QIT; ++i) {
+      const int q = tid + i * kLnThreads;
+      xv[i] = q < QN ? __builtin_nontemporal_load(xb + q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  int b = blockIdx.x;
+  if (b < B) load(b);
+  {  // zero the halo of the 16 planes once (k_leafnet_x3's map): every board writes only interiors
     constexpr int kHaloCols = RS - N, kHalo = 2 * RS + N * kHaloCols;
     for (int i = tid; i < 16 * kHalo; i += kLnThreads) {
       const int plane = i / kHalo, k = i - plane * kHalo;
@@ -72,71 +76,75 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_conv_x3(const float* __restri
   auto wload = [&](int c, int p) {
     return __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, l * 16, ((c * 8 + wave * 2 + p) * 64) * 16, 0));
   };
-  h16x8 wq[kLnWpf + 1][2];
-#pragma unroll
-  for (int c = 0; c < kLnWpf; ++c) {
-    wq[c][0] = wload(c, 0);
-    wq[c][1] = wload(c, 1);
-  }
   const f32x4 sv = *reinterpret_cast<const f32x4*>(inv + oc);
   const f32x4 bv = bias ? *reinterpret_cast<const f32x4*>(bias + oc) : f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // scale by the board maximum, split, into the planes: quad q of pixel p = channels 4q..4q+3,
-  // octet q/2 (hi plane 4 (o % 4) + 2 (o / 4), lo the next), half q % 2 of the octet's 16-B slot
-  float m = 0.0f;
-#pragma unroll
-  for (int i = 0; i < QIT; ++i) m = max3_abs(max3_abs(m, xv[i].x, xv[i].y), xv[i].z, xv[i].w);
-  const float max_in = block_max(m, red, wave, l);  // the barrier also orders the halo zeroing
-  const int ex = scale_exp(max_in);
-#pragma unroll
-  for (int i = 0; i < QIT; ++i) {
-    const int q = tid + i * kLnThreads;
-    if (q < QN) {
-      const int p = q >> 4, qq = q & 15, o = qq >> 1;
-      unsigned h0, h1, l0, l1;
-      split2(ldexpf(xv[i].x, ex), ldexpf(xv[i].y, ex), h0, l0);
-      split2(ldexpf(xv[i].z, ex), ldexpf(xv[i].w, ex), h1, l1);
-      unsigned char* d = act + ((o & 3) * 4 + (o >> 2) * 2) * PL + ((p / N + 1) * RS + p % N + 1) * 16 + (qq & 1) * 8;
-      *reinterpret_cast<u32x2*>(d) = u32x2{h0, h1};
-      *reinterpret_cast<u32x2*>(d + PL) = u32x2{l0, l1};
-    }
-  }
-  __syncthreads();
-
-  // the 18 chunks (tap c/2, channel half c%2), weights kLnWpf chunks ahead
-  f32x4 acc[NG];
-  h16x8 rb[kLnSlots][2];
   auto coff_of = [&](int c) {
     const int t = c >> 1;
     return 2 * (c & 1) * PL + ((t / 3 - 1) * RS + (t % 3 - 1)) * 16 + kBias;
   };
-  ln_prime<NG, PL>(rb, act, ab, coff_of(0));
-#pragma unroll
-  for (int c = 0; c < 18; ++c) {
-    const int cn = c + kLnWpf, sn = cn % (kLnWpf + 1);
-    if (cn < 18) {
-      wq[sn][0] = wload(cn, 0);
-      wq[sn][1] = wload(cn, 1);
-    }
-    const h16x8* wc = wq[c % (kLnWpf + 1)];
-    if (c == 0)
-      ln_chunk<NG, true, PL>(acc, wc[0], wc[1], act, ab, coff_of(0), coff_of(1), rb);
-    else
-      ln_chunk<NG, false, PL>(acc, wc[0], wc[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
-  }
-  ln_mfma_drain(acc);
 
-  // y = acc * inv * 2^-ex + bias, NHWC
-  const f32x2 s01{ldexpf(sv.x, -ex), ldexpf(sv.y, -ex)}, s23{ldexpf(sv.z, -ex), ldexpf(sv.w, -ex)};
-  const f32x2 b01{bv.x, bv.y}, b23{bv.z, bv.w};
-  float* yb = y + b * NN * 64;
+  for (; b < B; b += gridDim.x) {
+    h16x8 wq[kLnWpf + 1][2];
 #pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    if (is_valid(g)) {
-      const f32x2 y01 = pk_fma(f32x2{acc[g][0], acc[g][1]}, s01, b01);
-      const f32x2 y23 = pk_fma(f32x2{acc[g][2], acc[g][3]}, s23, b23);
-      __builtin_nontemporal_store(f32x4{y01.x, y01.y, y23.x, y23.y},
-                                  reinterpret_cast<f32x4*>(yb + ln_pixel<N>(slot_b(g) / 16) * 64 + oc));
+    for (int c = 0; c < kLnWpf; ++c) {
+      wq[c][0] = wload(c, 0);
+      wq[c][1] = wload(c, 1);
+    }
+    // scale by the board maximum, split, into the planes: quad q of pixel p = channels 4q..4q+3,
+    // octet q/2 (hi plane 4 (o % 4) + 2 (o / 4), lo the next), half q % 2 of the octet's 16-B slot
+    float m = 0.0f;
+#pragma unroll
+    for (int i = 0; i < QIT; ++i) m = max3_abs(max3_abs(m, xv[i].x, xv[i].y), xv[i].z, xv[i].w);
+    // the barrier in block_max also orders the halo zeroing and the previous board's grid reads
+    const float max_in = block_max(m, red + 4 * ((b / gridDim.x) & 1), wave, l);
+    const int ex = scale_exp(max_in);
+#pragma unroll
+    for (int i = 0; i < QIT; ++i) {
+      const int q = tid + i * kLnThreads;
+      if (q < QN) {
+        const int p = q >> 4, qq = q & 15, o = qq >> 1;
+        unsigned h0, h1, l0, l1;
+        split2(ldexpf(xv[i].x, ex), ldexpf(xv[i].y, ex), h0, l0);
+        split2(ldexpf(xv[i].z, ex), ldexpf(xv[i].w, ex), h1, l1);
+        unsigned char* d = act + ((o & 3) * 4 + (o >> 2) * 2) * PL + ((p / N + 1) * RS + p % N + 1) * 16 + (qq & 1) * 8;
+        *reinterpret_cast<u32x2*>(d) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(d + PL) = u32x2{l0, l1};
+      }
+    }
+    if (b + (int)gridDim.x < B) load(b + gridDim.x);  // the next board, in flight under this one's MFMAs
+    __syncthreads();
+
+    // the 18 chunks (tap c/2, channel half c%2), weights kLnWpf chunks ahead
+    f32x4 acc[NG];
+    h16x8 rb[kLnSlots][2];
+    ln_prime<NG, PL>(rb, act, ab, coff_of(0));
+#pragma unroll
+    for (int c = 0; c < 18; ++c) {
+      const int cn = c + kLnWpf, sn = cn % (kLnWpf + 1);
+      if (cn < 18) {
+        wq[sn][0] = wload(cn, 0);
+        wq[sn][1] = wload(cn, 1);
+      }
+      const h16x8* wc = wq[c % (kLnWpf + 1)];
+      if (c == 0)
+        ln_chunk<NG, true, PL>(acc, wc[0], wc[1], act, ab, coff_of(0), coff_of(1), rb);
+      else
+        ln_chunk<NG, false, PL>(acc, wc[0], wc[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+    }
+    ln_mfma_drain(acc);
+
+    // y = acc * inv * 2^-ex + bias, NHWC
+    const f32x2 s01{ldexpf(sv.x, -ex), ldexpf(sv.y, -ex)}, s23{ldexpf(sv.z, -ex), ldexpf(sv.w, -ex)};
+    const f32x2 b01{bv.x, bv.y}, b23{bv.z, bv.w};
+    float* yb = y + (size_t)b * NN * 64;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (is_valid(g)) {
+        const f32x2 y01 = pk_fma(f32x2{acc[g][0], acc[g][1]}, s01, b01);
+        const f32x2 y23 = pk_fma(f32x2{acc[g][2], acc[g][3]}, s23, b23);
+        __builtin_nontemporal_store(f32x4{y01.x, y01.y, y23.x, y23.y},
+                                    reinterpret_cast<f32x4*>(yb + ln_pixel<N>(slot_b(g) / 16) * 64 + oc));
+      }
     }
   }
 }
@@ -452,8 +460,9 @@ int bk_conv_x3(const float* x, int B, int N, const void* wsplit, const float* in
     const void* fns[1] = {(const void*)k_conv_x3<20>};
     if (set_max_dynamic_lds(fns, 1, ln_lds_bytes(20)) != BK_OK) return BK_EHIP;
   }
-  hipLaunchKernelGGL(k_conv_x3<20>, dim3(B), dim3(kLnThreads), ln_lds_bytes(20), (hipStream_t)stream, x,
-                     (const h16x8*)wsplit, inv, bias, y);
+  const int G = B < 256 ? B : 256;  // persistent: one workgroup per CU, boards strided
+  hipLaunchKernelGGL(k_conv_x3<20>, dim3(G), dim3(kLnThreads), ln_lds_bytes(20), (hipStream_t)stream, x,
+                     (const h16x8*)wsplit, inv, bias, y, B);
   return launch_check("k_conv_x3");
 }
 
