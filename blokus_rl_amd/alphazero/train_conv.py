@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 from ..engine import _check, _ptr, _stream, load_library
-from ..nets import use_native_batchnorm
+from ..nets import NativeBatchNorm2d, use_native_batchnorm
 
 
 def pack_weight(weight: torch.Tensor, flip: bool) -> tuple[torch.Tensor, torch.Tensor]:
@@ -94,6 +94,67 @@ class ConvX3Function(torch.autograd.Function):
         return gx, gw, gb
 
 
+class BatchNormFunction(torch.autograd.Function):
+    """Train-mode batch norm of a channels_last [B, 64, H, W] f32 activation on bk_bn_forward /
+    bk_bn_backward (fp64 statistics, one streaming read per reduction); updates the running
+    statistics in place like nn.BatchNorm2d."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        lib = load_library()
+        x = x.contiguous(memory_format=torch.channels_last)
+        M = x.numel() // 64
+        ws = torch.empty(lib.bk_bn_workspace_doubles(), dtype=torch.float64, device=x.device)
+        stats = torch.empty(256, dtype=torch.float32, device=x.device)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        _check(lib.bk_bn_forward(ctypes.c_void_p(x.data_ptr()), M, _ptr(weight), _ptr(bias), _ptr(running_mean),
+                                 _ptr(running_var), float(momentum), float(eps), _ptr(ws), _ptr(stats),
+                                 ctypes.c_void_p(y.data_ptr()), _stream(x.device)))
+        ctx.save_for_backward(x, weight, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = load_library()
+        x, weight, stats = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        M = x.numel() // 64
+        ws = torch.empty(lib.bk_bn_workspace_doubles(), dtype=torch.float64, device=x.device)
+        coef = torch.empty(256, dtype=torch.float32, device=x.device)
+        dg = torch.empty(64, dtype=torch.float32, device=x.device)
+        db = torch.empty(64, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        _check(lib.bk_bn_backward(ctypes.c_void_p(gy.data_ptr()), ctypes.c_void_p(x.data_ptr()), M, _ptr(weight),
+                                  _ptr(stats), _ptr(ws), _ptr(coef), _ptr(dg), _ptr(db), ctypes.c_void_p(dx.data_ptr()),
+                                  _stream(x.device)))
+        return dx, dg, db, None, None, None, None
+
+
+class FusedBatchNorm2d(NativeBatchNorm2d):
+    """nn.BatchNorm2d(64) (same parameters, buffers and state_dict keys) whose train-mode device
+    calls on 64-channel f32 activations run BatchNormFunction; everything else (eval mode, CPU,
+    other shapes, momentum=None) takes PyTorch's own batch norm."""
+
+    def forward(self, x):
+        if (self.training and x.is_cuda and x.dim() == 4 and x.shape[1] == 64 and x.dtype == torch.float32
+                and self.affine and self.track_running_stats and self.momentum is not None
+                and x.numel() > 64):
+            self.num_batches_tracked.add_(1)
+            return BatchNormFunction.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                           self.momentum, self.eps)
+        return super().forward(x)
+
+
+def use_fused_batchnorm(model: nn.Module) -> int:
+    """Switch every 64-channel BatchNorm2d of `model` to FusedBatchNorm2d in place."""
+    k = 0
+    for m in model.modules():
+        if type(m) in (nn.BatchNorm2d, NativeBatchNorm2d) and m.num_features == 64:
+            m.__class__ = FusedBatchNorm2d
+            k += 1
+    return k
+
+
 def _eligible(m: nn.Module) -> bool:
     return (type(m) is nn.Conv2d and m.in_channels == 64 and m.out_channels == 64 and m.kernel_size == (3, 3)
             and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1) and m.groups == 1
@@ -121,10 +182,13 @@ def use_x3_convs(model: nn.Module) -> int:
     return k
 
 
-def prepare_model(model: nn.Module, x3_convs: bool = True) -> nn.Module:
-    """The device training path in place: channels_last parameters, PyTorch batch norm, and
-    (x3_convs) the tower convs on bk_conv_x3."""
+def prepare_model(model: nn.Module, x3_convs: bool = True, fused_bn: bool = True) -> nn.Module:
+    """The device training path in place: channels_last parameters, PyTorch batch norm (the
+    64-channel ones on bk_bn_forward / bk_bn_backward when fused_bn), and (x3_convs) the tower
+    convs on bk_conv_x3."""
     use_native_batchnorm(model)
+    if fused_bn:
+        use_fused_batchnorm(model)
     if x3_convs:
         use_x3_convs(model)
     return model.to(memory_format=torch.channels_last)

@@ -70,6 +70,9 @@ _SIGS = {
     "bk_conv_x3": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "bk_conv_x3_wgrad_workspace_floats": (_i, [_i]),
     "bk_conv_x3_wgrad": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "bk_bn_workspace_doubles": (_i, []),
+    "bk_bn_forward": (_i, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "bk_bn_backward": (_i, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bk_ppo_gae": (_i, [_i, _i, _vp, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp]),
     "bk_filter_legal": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp]),
     "bk_bias_act": (_i, [_vp, ctypes.c_int64, _i, _vp, _vp, _i, _vp]),

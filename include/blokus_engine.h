@@ -286,6 +286,21 @@ int bk_conv_x3_pack(const float* w, int flip, void* wsplit, float* inv, void* st
 int bk_conv_x3(const float* x, int B, int N, const void* wsplit, const float* inv, const float* bias, float* y,
                void* stream);
 
+/* The learner's train-mode batch norm of a 64-channel NHWC activation x [M][64] f32 (M = batch
+ * x pixels; nn.BatchNorm2d(64) of models/blokus_nnet.py:99-112 in neural_network.py:52-85's
+ * train_step): batch mean / biased variance summed in fp64 (one read of x), y = (x - mean)
+ * gamma / sqrt(var + eps) + beta, running_mean / running_var updated in place as PyTorch does
+ * (momentum, unbiased variance; either may be NULL). stats [256] f32 receives mean, invstd,
+ * scale, shift (the backward's input); workspace: bk_bn_workspace_doubles() doubles. The
+ * backward: dx = dL/dx, dgamma, dbeta (may be NULL) from dy and x (one read of both for the
+ * sums, one pass for dx); coef [192] f32 scratch. gamma / beta may be NULL (1 / 0). */
+int bk_bn_workspace_doubles(void);
+int bk_bn_forward(const float* x, int64_t M, const float* gamma, const float* beta, float* running_mean,
+                  float* running_var, float momentum, float eps, double* workspace, float* stats, float* y,
+                  void* stream);
+int bk_bn_backward(const float* dy, const float* x, int64_t M, const float* gamma, const float* stats, double* workspace,
+                   float* coef, float* dgamma, float* dbeta, float* dx, void* stream);
+
 /* ---------------------------------------------------------------- PPO
  * PPOTrainer._compute_gae (ppo/trainer.py:177-211) + returns = advantages + values (:83) for a
  * rollout of T steps x E envs ([T][E] f32, row t = step t): float32, the reference's operation

@@ -135,6 +135,46 @@ def test_conv_x3_wgrad_fp32_class():
     assert torch.equal(conv_x3_wgrad(x32[:0], gy32[:0]), torch.zeros(64, 64, 3, 3, device="cuda"))
 
 
+def test_fused_batchnorm_matches_fp64():
+    """FusedBatchNorm2d (bk_bn_forward / bk_bn_backward) against nn.BatchNorm2d in fp64: the
+    output, the running statistics after two steps, and dx / dgamma / dbeta, to 2e-6 relative to
+    each quantity's scale; eval mode is PyTorch's own path."""
+    from blokus_rl_amd.alphazero.train_conv import FusedBatchNorm2d
+
+    g = torch.Generator().manual_seed(5)
+    ref = torch.nn.BatchNorm2d(64).double()
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5, generator=g)
+        ref.bias.uniform_(-0.3, 0.3, generator=g)
+    bn = torch.nn.BatchNorm2d(64).cuda()
+    bn.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
+    bn.__class__ = FusedBatchNorm2d
+    for step in range(2):
+        x = (torch.randn(37, 64, 20, 20, generator=g, dtype=torch.float64) * 3 + 5).float().double()
+        gy = torch.randn(37, 64, 20, 20, generator=g, dtype=torch.float64).float().double()
+        xr = x.clone().requires_grad_()
+        ref.train()
+        yr = ref(xr)
+        yr.backward(gy)
+        xd = x.float().cuda().contiguous(memory_format=torch.channels_last).requires_grad_()
+        bn.train()
+        y = bn(xd)
+        y.backward(gy.float().cuda().contiguous(memory_format=torch.channels_last))
+        assert float((y.detach().double().cpu() - yr.detach()).abs().max()) <= 2e-6 * float(yr.detach().abs().max())
+        assert float((xd.grad.double().cpu() - xr.grad).abs().max()) <= 2e-6 * float(xr.grad.abs().max())
+        for a, b in ((bn.weight.grad, ref.weight.grad), (bn.bias.grad, ref.bias.grad)):
+            assert float((a.double().cpu() - b).abs().max()) <= 2e-6 * float(b.abs().max())
+        bn.weight.grad = bn.bias.grad = None
+        ref.zero_grad()
+    for a, b in ((bn.running_mean, ref.running_mean), (bn.running_var, ref.running_var)):
+        assert float((a.double().cpu() - b).abs().max()) <= 2e-6 * float(b.abs().max())
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 2
+    bn.eval()
+    ref.eval()
+    x = torch.randn(3, 64, 20, 20, generator=g, dtype=torch.float64)
+    assert torch.allclose(bn(x.float().cuda()).double().cpu(), ref(x), atol=1e-5, rtol=1e-5)
+
+
 def test_conv_x3_rejects_bad_shapes():
     from blokus_rl_amd.alphazero.train_conv import conv_x3, pack_weight
 
@@ -159,7 +199,10 @@ def _replay(n=512):
 
 def test_learner_device_path_gradients_match_fp32():
     """One training step's gradients (the reference's compute_loss through the whole ResNet) on the
-    device path against the fp32 path, parameter by parameter: within 1e-4 of the gradient's norm.
+    device path against the fp32 path, parameter by parameter: within 5e-4 of the gradient's norm
+    (the fp32 path's own error: its batch-norm parameter gradients are f32 sums over 102k terms
+    that largely cancel, ~1e-4 of their norm off the fp64 value; the device path sums in fp64 and
+    is checked against fp64 directly in test_fused_batchnorm_matches_fp64).
     The biases of the convs that feed a batch norm are left out: under train-mode batch norm their
     gradient is zero in exact arithmetic (the channel mean is subtracted), so both paths return
     rounding noise."""
@@ -184,7 +227,7 @@ def test_learner_device_path_gradients_match_fp32():
                 k.startswith("res_blocks") and k.endswith(".bias") and k.split(".")[2] in ("0", "3")):
             continue  # the bias of a conv that feeds a batch norm: zero in exact arithmetic
         d = (grads[True][k] - g32).norm()
-        assert float(d) <= 1e-4 * float(g32.norm()) + 1e-12, (k, float(d), float(g32.norm()))
+        assert float(d) <= 5e-4 * float(g32.norm()) + 1e-12, (k, float(d), float(g32.norm()))
 
 
 def test_learner_device_path_tracks_fp32():
