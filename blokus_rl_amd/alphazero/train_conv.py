@@ -1,6 +1,7 @@
 """The learner's device path for the ResNet: the residual tower's 3x3
-convolutions 64 -> 64 on the f16 matrix cores (bk_conv_x3: split-f16 products, fp32-class), the
-activations in channels_last (NHWC) and batch norm on PyTorch's own kernels.
+convolutions 64 -> 64 on the f16 matrix cores (bk_conv_x3 / bk_conv_x3_wgrad: split-f16 products,
+fp32-class), the activations in channels_last (NHWC), the 64-channel train-mode batch norms on
+bk_bn_forward / bk_bn_backward (fp64 statistics) and the heads' small ones on PyTorch's kernels.
 
 The reference trains models/blokus_nnet.py:88-151 in fp32 (neural_network.py:52-85); on MI355X
 the fp32 convolutions (MIOpen igemm / Winograd on the f32 MFMA, 1/16 of the f16 rate on gfx950)
