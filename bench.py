@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 from blokus_rl_amd.replay import dist_active  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
+MFMA_F16_PEAK = 2.5e15  # FLOP/s, dense f16 MFMA (MI355X_MICROARCH.md; not the 2:1-sparsity figure)
 
 # Algorithmic bytes of one board in k_legal_mask: the packed state read (384 B) + the
 # 30433-bit mask written (476 u64 = 3808 B) + its count (4 B). DESIGN.md §4.
@@ -639,6 +640,15 @@ def bench_train(args, world, rank):
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk["achieved_GBps"] * 1e9 / HBM_PEAK,
                         "kernel_ms": lk["ms"], "bytes_per_launch_pair": lk["bytes_per_launch_pair"],
                         "units_per_launch": args.train_batch, "traffic": None}}
+    if "conv_kernel" in main_r:  # the device path's dominant kernel: k_conv_x3 on the f16 matrix cores
+        ck = main_r["conv_kernel"]
+        out["loss_roofline"] = out["roofline"]
+        out["roofline"] = {"bound": "mfma", "kernel": ck["kernel"], "achieved": ck["flop"] / (ck["ms"] * 1e-3) / 1e12,
+                           "peak": MFMA_F16_PEAK / 1e12, "unit": "TFLOP/s",
+                           "frac": ck["flop"] / (ck["ms"] * 1e-3) / MFMA_F16_PEAK, "kernel_ms": ck["ms"],
+                           "flop_per_launch": ck["flop"], "units_per_launch": args.train_batch, "traffic": None,
+                           "fp32_equiv_tflops": ck["fp32_equiv_flop"] / (ck["ms"] * 1e-3) / 1e12,
+                           "note": "executed split-f16 MFMA work (3 f16 products per fp32 product)"}
     if "reference_path" in res["b64"]:
         out["reference_path_batch_64"] = res["b64"]["reference_path"]
     return out

@@ -69,6 +69,30 @@ def time_loss_kernels(x, ids, pi, k, reps: int = 50):
     return e0.elapsed_time(e1) / reps
 
 
+def time_conv_x3(batch: int, device, reps: int = 20) -> dict:
+    """k_conv_x3 alone at the learner's batch (HIP events on the stream it launches on): its
+    executed MFMA work per launch = batch x 4 waves x 25 pixel groups x 18 K-chunks x 3 products
+    of v_mfma_f32_16x16x32_f16 (16384 FLOP each); the fp32-equivalent conv = 2 x batch x 400 x 64 x 576."""
+    from .train_conv import conv_x3, pack_weight
+
+    g = torch.Generator(device=device).manual_seed(0)
+    x = torch.randn(batch, 64, 20, 20, device=device, generator=g).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(64, 64, 3, 3, device=device, generator=g) * 0.06
+    ws, inv = pack_weight(w, False)
+    for _ in range(3):
+        conv_x3(x, ws, inv, None)
+    st = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        conv_x3(x, ws, inv, None)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"kernel": "k_conv_x3", "ms": ms, "flop": float(batch) * 4 * 25 * 18 * 3 * 16384,
+            "fp32_equiv_flop": 2.0 * batch * 400 * 64 * 576}
+
+
 def reference_loop_loss(masks, p_pred, v_pred, p_gt, v_gt):
     """compute_loss as written in neural_network.py:138-157 (per-sample loop)."""
     v_loss = (v_pred.squeeze() - v_gt).pow(2).mean()
@@ -156,6 +180,8 @@ def bench_learner(eng, world: int, rank: int, batch: int, steps: int, warmup: in
     out = {"batch_per_gpu": batch, "steps": steps, "elapsed_s": dt, "loss": float(loss), "device_path": L.device_path,
            "loss_kernels": {"kernel": "k_policy_loss + k_policy_loss_grad", "ms": kms,
                             "bytes_per_launch_pair": kbytes, "achieved_GBps": kbytes / (kms * 1e-3) / 1e9}}
+    if L.device_path:
+        out["conv_kernel"] = time_conv_x3(batch, eng.device)
     if reference_steps and rank == 0 and world == 1:
         ref_model = ResNet(eng.N, eng.P, eng.A, 5).to(eng.device)
         out["reference_path"] = bench_reference_path(eng, states, ids, pi, k, z, batch, reference_steps, ref_model)
