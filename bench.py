@@ -179,22 +179,26 @@ def bench_dry(args, world, rank):
 
 
 def _pmc_traffic(kernel_prefix: str, units_per_launch: int, with_source: bool = False):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json) of this
+    """HBM bytes per launch from the committed rocprofv3 PMC summaries (profiles/*pmc*.json) of this
     kernel at this launch size, FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md
-    §HBM); the newest file (by name: rNN_ prefix) wins. None when absent. with_source: (bytes,
-    the profile's file name) — a committed measurement, not one of this run."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    for fp in reversed(files):
+    §HBM). Among the files holding the kernel at that size, the one with the highest "round" field
+    wins (file names break ties only within a round). None when absent. with_source: (bytes, the
+    profile's file name) — a committed measurement, not one of this run."""
+    best = None
+    for fp in glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")):
         try:
             with open(fp, encoding="utf-8") as f:
                 d = json.load(f)
             k = d.get("kernels", {}).get(kernel_prefix)
             if k and k.get("units_per_launch") == units_per_launch:
-                v = float(k["hbm_bytes_per_launch"])
-                return (v, os.path.basename(fp)) if with_source else v
+                rank = (int(d.get("round", 0)), os.path.basename(fp))
+                if best is None or rank > best[0]:
+                    best = (rank, float(k["hbm_bytes_per_launch"]), os.path.basename(fp))
         except Exception:
             continue
-    return (None, None) if with_source else None
+    if best is None:
+        return (None, None) if with_source else None
+    return (best[1], best[2]) if with_source else best[1]
 
 
 # ----------------------------------------------------------------------------- CPU baselines
@@ -491,19 +495,57 @@ def bench_vecenv(args, world, rank):
         env.step(None)
     torch.cuda.synchronize()
     eager = E * 200 / (time.perf_counter() - te)
-    # PPO-style: the agent's actions sampled on the device from masked logits each step
-    logits = torch.zeros((E, env.eng.A), device=env.device)
-    for _ in range(5):
-        a = torch.distributions.Categorical(logits=env.masked_logits(logits)).sample()
-        env.step(a)
+    # PPO-style: the agent's actions drawn from policy logits each step (the rollout's
+    # get_action_and_value + env.step, ppo/trainer.py:144-155) — bk_vec_policy (FilterLegalMoves +
+    # Categorical sample + log_prob in one launch) then k_vec_step7, replayed from a HIP graph of
+    # `per` such pairs; the logits row is the actor's output stand-in (random, [E, A] f32 in HBM)
+    logits = (torch.randn((E, env.eng.A), device=env.device, generator=torch.Generator(env.device).manual_seed(rank))
+              * 2.0).contiguous()
+    gp, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gp):
+        for _ in range(per):
+            env.step_policy(logits)
+    with torch.cuda.graph(gs):  # the draw alone (its kernel time for the roofline)
+        for _ in range(per):
+            env.sample_policy(logits)
+    gp.replay()
+    gs.replay()
     torch.cuda.synchronize()
+    reps2 = max(1, args.vec_steps // per)
+    _barrier(world)
     t1 = time.perf_counter()
-    n2 = max(10, args.vec_steps // 10)
-    for _ in range(n2):
-        a = torch.distributions.Categorical(logits=env.masked_logits(logits)).sample()
-        env.step(a)
+    e0.record(stream)
+    for _ in range(reps2):
+        gp.replay()
+    e1.record(stream)
     torch.cuda.synchronize()
-    dt2 = time.perf_counter() - t1
+    _barrier(world)
+    dt2 = _max_over_ranks(time.perf_counter() - t1, world)
+    pair_ms = e0.elapsed_time(e1) / (reps2 * per)
+    e0.record(stream)
+    for _ in range(reps2):
+        gs.replay()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    pol_ms = e0.elapsed_time(e1) / (reps2 * per)
+    n2 = reps2 * per
+    # the same draw as generic torch ops (the round-5 path): unpack the mask, -1e9 fill,
+    # Categorical sample + log_prob, then env.step — for comparison only
+    def torch_step():
+        dist_t = torch.distributions.Categorical(logits=env.masked_logits(logits))
+        a_t = dist_t.sample()
+        dist_t.log_prob(a_t)
+        env.step(a_t)
+
+    for _ in range(3):
+        torch_step()
+    torch.cuda.synchronize()
+    tt = time.perf_counter()
+    for _ in range(50):
+        torch_step()
+    torch.cuda.synchronize()
+    torch_ops = E * 50 / (time.perf_counter() - tt)
+    pol_bytes = 4 * env.eng.A + 8 * env.eng.W + 16 + 8
     achieved = VEC_BYTES_PER_STEP * E / (kernel_ms * 1e-3)
     # the headline is the DEVICE rate (graph-replayed launches, in-kernel agent draws); a gym-style
     # loop calling env.step() per step gets eager_env_step_calls (one launch + tensor bookkeeping
@@ -515,10 +557,22 @@ def bench_vecenv(args, world, rank):
            "byte_accounting": "bytes_per_unit counts the state words a 7x7 game uses (393 B since round 4; "
                               "round 3 counted the whole 384-B state each way, 965 B): fractions are not "
                               "comparable with rounds <= 3",
-           "with_masked_policy_sampling": {"value": E * n2 / dt2, "unit": "env-steps/s"},
+           "with_masked_policy_sampling": {
+               "value": E * n2 * world / dt2, "unit": "env-steps/s", "steps": n2,
+               "path": "bk_vec_policy (FilterLegalMoves + Categorical sample + log_prob, one launch) -> k_vec_step7, "
+                       "HIP-graph-replayed pairs; logits [E, A] f32 resident in HBM (the actor's output stand-in)",
+               "ms_per_step": pair_ms,
+               "roofline": {"bound": "hbm", "kernel": "k_vec_policy", "achieved": pol_bytes * E / (pol_ms * 1e-3) / 1e9,
+                            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": pol_bytes * E / (pol_ms * 1e-3) / HBM_PEAK,
+                            "kernel_ms": pol_ms, "bytes_per_unit": pol_bytes, "units_per_launch": E,
+                            "traffic": _pmc_traffic("k_vec_policy", E)},
+               "torch_ops_eager": {"value": torch_ops, "unit": "env-steps/s",
+                                   "note": "round-5 path: valid_mask + torch.where(-1e9) + Categorical.sample/log_prob + "
+                                           "env.step per step"}},
            "roofline": {"bound": "hbm", "kernel": "k_vec_step7", "achieved": achieved / 1e9,
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                        "kernel_ms": kernel_ms, "bytes_per_unit": VEC_BYTES_PER_STEP, "units_per_launch": E}}
+                        "kernel_ms": kernel_ms, "bytes_per_unit": VEC_BYTES_PER_STEP, "units_per_launch": E,
+                        "traffic": _pmc_traffic("k_vec_step7", E)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_vecenv(args.cpu_seconds / 2, args.cpu_pool, args.cpu_workers)
     return out

@@ -590,6 +590,133 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   VSTAMP(7);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_vec_policy: the agent's move drawn from its policy, as the reference's PPO rollout draws it
+// (ppo/trainer.py:144-155 -> CnnAgent.get_action_and_value, ppo/agent.py:148-156: the actor's
+// logits through FilterLegalMoves, :27-42, then Categorical(logits).sample() and .log_prob()).
+// One wave per env: lane l loads ids 64 t + l (t < T), one coalesced 256-B row segment per load;
+// mask word t is wave-uniform (a scalar load), so a lane's candidate test is one bit of it. The
+// candidates are the legal ids (minus those whose logit is exactly 0 under the reference filter's
+// quirk); with none, every id in [0, A) at logit -1e9 (the reference's all -1e9 row: uniform).
+// The K candidates are compacted in ascending id order into the wave's LDS slots (mask word +
+// mbcnt rank; ~22 of 919 ids on the config-5 boards, mostly one slot per lane),
+// so the exponentials run on K / 64 slots per lane instead of all T x 64 ids (VALU-bound
+// otherwise: ~8 % of a 7x7 row is legal). The draw is an inverse CDF with a fixed, restatable
+// arithmetic (oracle/vecenv_oracle.py policy_sample):
+//   m = max candidate logit; p_j = bk_expf(x_j - m) for slot j; s_l = sum over slots l, l + 64,
+//   ... in order; incl = BK_WAVE_SCAN of s (DPP order); S = incl_63; u = (z >> 40) 2^-24 from the
+//   env's splitmix64 stream (one draw; the env's own stream, as the opponent's moves);
+//   target = S u; lane = first with incl > target (else the last with s > 0); walking its slots
+//   from incl_{lane-1}: the first whose running sum passes the target (else its last p > 0);
+//   logp = x_a - (m + bk_logf(S))  (torch's logsumexp form, so the all -1e9 row gives 0 as there).
+// Bound: HBM (the [E][A] f32 logits row, 4 B per id).
+// exp / log from + - * / only (-ffp-contract=off): bitwise reproducible by numpy float32.
+__device__ __forceinline__ float bk_expf(float x) {  // x <= 0; below -80 (e^-80 < 2^-115): 0
+  if (!(x >= -80.0f)) return 0.0f;
+  const float n = __builtin_rintf(x * 1.44269502f);
+  const float r = (x - n * 0.693145752f) - n * 1.42860677e-6f;
+  float p = 1.38888892e-3f;
+  p = p * r + 8.33333377e-3f;
+  p = p * r + 4.16666679e-2f;
+  p = p * r + 0.166666672f;
+  p = p * r + 0.5f;
+  p = p * r + 1.0f;
+  p = p * r + 1.0f;
+  return p * __int_as_float(((int)n + 127) << 23);
+}
+__device__ __forceinline__ float bk_logf(float x) {  // x >= 1, finite
+  const int bits = __float_as_int(x);
+  int e = ((bits >> 23) & 255) - 127;
+  float f = __int_as_float((bits & 0x7FFFFF) | 0x3F800000);  // [1, 2)
+  if (f > 1.41421354f) {
+    f = f * 0.5f;
+    e += 1;
+  }
+  const float s = (f - 1.0f) / (f + 1.0f);
+  const float s2 = s * s;
+  float q = 0.111111112f;
+  q = q * s2 + 0.142857149f;
+  q = q * s2 + 0.200000003f;
+  q = q * s2 + 0.333333343f;
+  q = q * s2 + 1.0f;
+  return (float)e * 0.693147182f + (2.0f * s) * q;
+}
+
+template <int T, int AC, bool ZQ>  // AC: the id count at compile time (the 7x7 presets), 0 = runtime A
+__global__ __launch_bounds__(256) void k_vec_policy(const float* __restrict__ logits, int A_, int W64_,
+                                                    const uint64_t* __restrict__ mask, uint64_t* __restrict__ rng,
+                                                    int E, int32_t* __restrict__ act, float* __restrict__ logp) {
+  const int A = AC ? AC : A_, W64 = AC ? (AC + 63) / 64 : W64_;
+  extern __shared__ __attribute__((aligned(16))) float pol_lds[];
+  float* xs = pol_lds + (threadIdx.x >> 6) * (T * 64);                                                // slot logits
+  uint16_t* is = reinterpret_cast<uint16_t*>(pol_lds + 4 * T * 64) + (threadIdx.x >> 6) * (T * 64);  // slot ids
+  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+  if (e >= E) return;  // wave-uniform
+  const int l = lane_id();
+  const float* row = logits + (size_t)e * A;
+  const uint64_t* mw = mask + (size_t)e * W64;
+  uint64_t st = rng[e];
+  float x[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) x[t] = (t < W64 && 64 * t + l < A) ? row[64 * t + l] : 0.0f;
+  // compaction, word by word: the candidates of word t are the mask word itself (wave-uniform,
+  // in SGPRs) limited to ids < A (and, under the quirk, to lanes whose logit is not 0); a zero
+  // word costs a scalar test only. Slot K + rank (mbcnt) gets (logit, id).
+  int K = 0;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int lim = A - 64 * t;
+    uint64_t b = t < W64 ? mw[t] : 0ull;
+    b &= lim >= 64 ? ~0ull : (lim > 0 ? (1ull << lim) - 1ull : 0ull);
+    if (b != 0ull) {  // wave-uniform
+      if (ZQ) b &= __ballot(x[t] != 0.0f);
+      if ((b >> l) & 1ull) {
+        const int j = K + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        xs[j] = x[t];
+        is[j] = (uint16_t)(64 * t + l);
+      }
+      K += __popcll(b);
+    }
+  }
+  const bool none = K == 0;  // no candidate: the all -1e9 row, slot j = id j (no LDS)
+  if (none) K = A;
+  wave_lds_sync();
+  float m = -INFINITY;
+  for (int j = l; j < K; j += kWave) m = fmaxf(m, none ? -1e9f : xs[j]);
+  m = wave_max_f(m);
+  float s = 0.0f;
+  for (int j = l; j < K; j += kWave) s = s + bk_expf((none ? -1e9f : xs[j]) - m);
+  float incl = s;
+  BK_WAVE_SCAN(incl, dpp_f, op_add_f);
+  const float S = readlane_f(incl, kWave - 1);
+  const uint64_t z = mix64(st);  // = the env's splitmix64 output (rng_index's draw)
+  st += 0x9E3779B97F4A7C15ull;
+  const float target = S * ((float)(uint32_t)(z >> 40) * 0x1p-24f);
+  const uint64_t over = __ballot(incl > target), pos = __ballot(s > 0.0f);
+  const int sel = over ? __ffsll((unsigned long long)over) - 1 : (pos ? 63 - __clzll((long long)pos) : 0);
+  const float excl = sel > 0 ? readlane_f(incl, sel - 1) : 0.0f;
+  if (l == sel) {
+    float acc = excl;
+    int pick = -1, last = -1;
+    for (int j = l; j < K; j += kWave) {
+      const float p = bk_expf((none ? -1e9f : xs[j]) - m);
+      if (p > 0.0f) {
+        acc = acc + p;
+        last = j;
+        if (acc > target) {
+          pick = j;
+          break;
+        }
+      }
+    }
+    if (pick < 0) pick = last;
+    // pick < 0 only for non-finite logits: an out-of-range id (the env's illegal-move loss)
+    act[e] = pick < 0 ? A : (none ? pick : (int)is[pick]);
+    logp[e] = pick < 0 ? __int_as_float(0x7FC00000) : (none ? -1e9f : xs[pick]) - (m + bk_logf(S));
+    rng[e] = st;
+  }
+}
+
 }  // namespace
 }  // namespace bk
 
@@ -644,6 +771,33 @@ int bk_vec_step(bk_ctx* c, void* states, uint64_t* rng, const int32_t* actions, 
   hipLaunchKernelGGL(k_vec_step, dim3(E), dim3(kWave), vec_lds(c->dp), (hipStream_t)stream, c->dp,
                      (uint32_t*)states, rng, actions, obs, mask, reward, done);
   return launch_check("k_vec_step");
+}
+
+int bk_vec_policy(bk_ctx* c, const float* logits, const uint64_t* mask, uint64_t* rng, int E, int zero_masked,
+                  int32_t* actions, float* logp, void* stream) {
+  BK_REQUIRE(c && logits && mask && rng && actions && logp && E >= 0, "bad argument");
+  BK_REQUIRE(c->dp.W64 <= 64, "policy sampling holds <= 64 x 64 ids per env (the 2-player 7x7 presets)");
+  if (E == 0) return BK_OK;
+  const dim3 grid((E + 3) / 4), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  const int A = c->dp.A, W = c->dp.W64;
+  // per wave: T x 64 slots of (f32 logit, u16 id)
+#define BK_POL(T, AC)                                                                                        \
+  if (zero_masked)                                                                                           \
+    hipLaunchKernelGGL((k_vec_policy<T, AC, true>), grid, block, 4 * (T) * 64 * 6, st, logits, A, W, mask, rng, \
+                       E, actions, logp);                                                                     \
+  else                                                                                                       \
+    hipLaunchKernelGGL((k_vec_policy<T, AC, false>), grid, block, 4 * (T) * 64 * 6, st, logits, A, W, mask, rng, \
+                       E, actions, logp)
+  if (A == 919) {
+    BK_POL(15, 919);
+  } else if (A == 2522) {
+    BK_POL(40, 2522);
+  } else {
+    BK_POL(64, 0);
+  }
+#undef BK_POL
+  return launch_check("k_vec_policy");
 }
 
 }  // extern "C"

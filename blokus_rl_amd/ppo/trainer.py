@@ -1,7 +1,9 @@
 """PPO trainer (blokus_rl/ppo/trainer.py:20-400) on the device vector env (config 5).
 
 Rollouts never leave the GPU: BlokusVectorEnv steps all envs in one kernel and hands back the
-agent's legal-move bitmask, which FilterLegalMoves applies in one kernel; GAE is one kernel over
+agent's legal-move bitmask; the rollout's draw (FilterLegalMoves + Categorical sample + log_prob of
+get_action_and_value, ppo/agent.py:27-42, 148-156) is one kernel over the actor's raw logits and
+that bitmask (bk_vec_policy; `device_sampling=False` keeps the torch Categorical path); GAE is one kernel over
 the [T, E] rollout (bk_ppo_gae, the reference's float32 operation order). The update
 (`optimize_agent`) is the reference's clipped-surrogate PPO step — same minibatch order (it
 draws its shuffles from np.random exactly as the reference does, so a seeded run matches),
@@ -157,8 +159,9 @@ def optimize_agent(agent: nn.Module, optimizer, batch: dict, hp) -> dict:
 class PPOTrainer:
     """PPOTrainer (trainer.py:20-400) with the device vector env instead of SyncVectorEnv."""
 
-    def __init__(self, hparams: PPOHparams, device: str | torch.device | None = None):
+    def __init__(self, hparams: PPOHparams, device: str | torch.device | None = None, device_sampling: bool = True):
         self.hparams = hp = hparams
+        self.device_sampling = device_sampling
         self.envs = BlokusVectorEnv(hp.num_envs, hp.board_size, hp.max_piece_cells, device=device)
         self.device = self.envs.device
         self.obs_shape = (hp.board_size, hp.board_size)
@@ -186,9 +189,16 @@ class PPOTrainer:
             m.obs[step] = next_obs
             m.dones[step] = next_done
             with torch.inference_mode():
-                action, logproba, _, value = self.agent.get_action_and_value(
-                    next_obs, possible_moves=self.envs.mask_words)
+                if self.device_sampling:
+                    h = self.agent.features(next_obs)
+                    logits = self.agent.actor(h).float().contiguous()  # raw: the filter runs in the draw
+                    value = self.agent.critic(h)
+                else:
+                    action, logproba, _, value = self.agent.get_action_and_value(
+                        next_obs, possible_moves=self.envs.mask_words)
                 m.values[step] = value.flatten()
+            if self.device_sampling:
+                action, logproba = self.envs.sample_policy(logits, zero_masked=True)
             m.actions[step] = action
             m.logprobs[step] = logproba
             obs, reward, term, _, _ = self.envs.step(action)

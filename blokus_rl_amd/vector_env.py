@@ -31,6 +31,8 @@ class BlokusVectorEnv:
         self.mask_words = torch.empty((E, self.eng.W), dtype=torch.int64, device=dev)
         self.reward = torch.zeros(E, dtype=torch.float32, device=dev)
         self.done = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.actions = torch.zeros(E, dtype=torch.int32, device=dev)  # bk_vec_policy's draws
+        self.logp = torch.zeros(E, dtype=torch.float32, device=dev)
 
     def _s(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -63,6 +65,28 @@ class BlokusVectorEnv:
         _check(self.eng.lib.bk_vec_step(self.eng.h, _ptr(self.states), _ptr(self.rng), _ptr(act), self.num_envs,
                                         _ptr(self.obs), _ptr(self.mask_words), _ptr(self.reward), _ptr(self.done),
                                         self._s()))
+
+    def sample_policy(self, logits: torch.Tensor, zero_masked: bool = True):
+        """The agent's moves drawn from its policy on the device (bk_vec_policy): the rollout's
+        `get_action_and_value(obs, possible_moves=...)` sample + log_prob (ppo/agent.py:148-156)
+        over FilterLegalMoves (:27-42; zero_masked = its rule that a legal logit of exactly 0 is
+        masked too) in one launch, from the actor's raw logits [E, A] f32 and the env's current
+        legal-move bitmask. Returns (actions [E] int32, logp [E] f32), updated in place
+        (capturable in a HIP graph: the checks are host-side)."""
+        E, A = self.num_envs, self.eng.A
+        if not (logits.is_cuda and logits.device == torch.device(self.device) and logits.dtype == torch.float32
+                and logits.is_contiguous() and tuple(logits.shape) == (E, A)):
+            raise ValueError(f"sample_policy wants contiguous float32 logits [{E}, {A}] on the env's device")
+        _check(self.eng.lib.bk_vec_policy(self.eng.h, _ptr(logits), _ptr(self.mask_words), _ptr(self.rng), E,
+                                          int(bool(zero_masked)), _ptr(self.actions), _ptr(self.logp), self._s()))
+        return self.actions, self.logp
+
+    def step_policy(self, logits: torch.Tensor, zero_masked: bool = True):
+        """One rollout step on the device: sample_policy, then step_raw with its actions (two
+        launches, no host round trip). Returns (actions, logp) of the step."""
+        self.sample_policy(logits, zero_masked)
+        self.step_raw(self.actions)
+        return self.actions, self.logp
 
     def valid_mask(self) -> torch.Tensor:
         """[E, A] bool: the agent's legal ids (the reference's ai_possible_indexes as a mask)."""

@@ -237,6 +237,19 @@ int bk_vec_reset(bk_ctx* ctx, void* states, uint64_t* rng, const uint64_t* seeds
                  uint64_t* mask, void* stream);
 int bk_vec_step(bk_ctx* ctx, void* states, uint64_t* rng, const int32_t* actions, int E, uint8_t* obs,
                 uint64_t* mask, float* reward, int32_t* done, void* stream);
+/* bk_vec_policy: the agent's moves drawn from its policy, as the PPO rollout draws them
+ * (ppo/trainer.py:144-155 -> get_action_and_value, ppo/agent.py:148-156: the actor's logits
+ * through FilterLegalMoves, :27-42, then Categorical(logits).sample() / .log_prob()), replacing
+ * the [E][A] filter + softmax + multinomial of that call. logits [E][A] f32 (the actor's raw
+ * output), mask [E][mask_words] (the agent's legal ids, as bk_vec_reset / bk_vec_step leave
+ * them). Candidates: the legal ids, minus those whose logit is exactly 0 when zero_masked != 0
+ * (the reference filter's quirk); with none, every id in [0, A) at -1e9 (uniform, as the
+ * reference's all -1e9 row). actions[e] is drawn from the softmax over the candidates by an
+ * inverse CDF on the env's splitmix64 stream (one draw; rng[e] advanced), logp[e] =
+ * logits[e][a] - logsumexp (Categorical.log_prob). Feed actions to bk_vec_step. 2-player 7x7
+ * presets (<= 4096 ids). */
+int bk_vec_policy(bk_ctx* ctx, const float* logits, const uint64_t* mask, uint64_t* rng, int E, int zero_masked,
+                  int32_t* actions, float* logp, void* stream);
 
 /* ---------------------------------------------------------------- learner
  * Packed replay row (blokus_rl_amd/replay.py), fixed stride bk_replay_stride(cap), 16-B aligned:

@@ -1,7 +1,12 @@
 """TEST INFRASTRUCTURE ONLY — CPU restatement of the config-5 vector env (one env at a time),
 the same rules (oracle/blokus_oracle.c) and the same per-env random stream as
 blokus_rl_amd/csrc/vecenv.hip, so the two compare bit for bit. The env restates blokus_gym
-`blokus-simple-v0` as the reference PPO uses it (ppo/trainer.py:128-175; docs/README.md:47-51)."""
+`blokus-simple-v0` as the reference PPO uses it (ppo/trainer.py:128-175; docs/README.md:47-51).
+
+`policy_sample` restates k_vec_policy (the rollout's masked-policy draw, ppo/agent.py:27-42 +
+:148-156, ppo/trainer.py:144-155) in numpy float32 with the kernel's exact operation order: its
+exp / log polynomials, per-lane sums, the DPP scan order of BK_WAVE_SCAN and the inverse-CDF
+walk, so actions and log-probs compare bit for bit."""
 from __future__ import annotations
 
 import numpy as np
@@ -9,10 +14,132 @@ import numpy as np
 from .oracle import Oracle
 
 M64 = (1 << 64) - 1
+GOLDEN = 0x9E3779B97F4A7C15
+F32 = np.float32
+
+
+def mix64(x: int) -> int:
+    """splitmix64 finalizer of x + golden (common.h mix64)."""
+    z = (x + GOLDEN) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def bk_expf(x):
+    """vecenv.hip bk_expf: x <= 0 in float32; 0 below -80."""
+    x = np.asarray(x, dtype=F32)
+    ok = x >= F32(-80.0)
+    xc = np.where(ok, x, F32(0))
+    n = np.rint(xc * F32(1.44269502))
+    r = (xc - n * F32(0.693145752)) - n * F32(1.42860677e-6)
+    p = np.full_like(r, F32(1.38888892e-3))
+    for c in (8.33333377e-3, 4.16666679e-2, 0.166666672, 0.5, 1.0, 1.0):
+        p = p * r + F32(c)
+    pw = ((n.astype(np.int32) + 127) << 23).astype(np.int32).view(F32)
+    return np.where(ok, p * pw, F32(0)).astype(F32)
+
+
+def bk_logf(x):
+    """vecenv.hip bk_logf: x >= 1 finite, float32."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=F32))
+    bits = x.view(np.int32)
+    e = ((bits >> 23) & 255) - 127
+    f = ((bits & 0x7FFFFF) | 0x3F800000).astype(np.int32).view(F32)
+    big = f > F32(1.41421354)
+    f = np.where(big, f * F32(0.5), f).astype(F32)
+    e = np.where(big, e + 1, e)
+    s = (f - F32(1)) / (f + F32(1))
+    s2 = s * s
+    q = np.full_like(s, F32(0.111111112))
+    for c in (0.142857149, 0.200000003, 0.333333343, 1.0):
+        q = q * s2 + F32(c)
+    return (e.astype(F32) * F32(0.693147182) + (F32(2) * s) * q).astype(F32)
+
+
+def wave_scan_f32(s):
+    """common.h BK_WAVE_SCAN with op_add_f over the 64 lanes of s [..., 64]: row_shr 1/2/4/8 inside
+    each row of 16, then row_bcast:15 (rows 1 and 3 add lane 15 of the row below) and
+    row_bcast:31 (lanes >= 32 add lane 31)."""
+    x = np.array(s, dtype=F32)
+    lane = np.arange(64)
+    for d in (1, 2, 4, 8):
+        src = x.copy()
+        sel = (lane & 15) >= d
+        x[..., sel] = src[..., lane[sel] - d] + src[..., sel]
+    src = x.copy()
+    sel = (lane & 31) >= 16
+    x[..., sel] = src[..., (lane[sel] // 16) * 16 - 1] + src[..., sel]
+    src = x.copy()
+    sel = lane >= 32
+    x[..., sel] = src[..., 31:32] + src[..., sel]
+    return x
+
+
+def policy_sample(logits, masks, rng, zero_masked: bool = True):
+    """k_vec_policy on the CPU. logits [E, A] f32, masks [E, W] u64 (the agent's legal ids), rng: E
+    int states. -> (actions int32 [E], logp f32 [E], new rng states). Per env: the candidates in
+    ascending id order are slots j = 0..K-1; lane l sums slots l, l + 64, ... in order."""
+    logits = np.asarray(logits, dtype=F32)
+    masks = np.asarray(masks, dtype=np.uint64)
+    E, A = logits.shape
+    W = masks.shape[1]
+    ids = np.arange(A)
+    bits = ((masks[:, ids // 64] >> (ids % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)  # [E, A]
+    cand = bits & ((logits != 0) if zero_masked else True)
+    none = ~cand.any(axis=1)
+    X = logits.copy()
+    X[none] = F32(-1e9)
+    cand[none] = True
+    m = np.where(cand, X, F32(-np.inf)).max(axis=1).astype(F32)
+    K = cand.sum(axis=1)
+    Kmax = int(K.max())
+    nk = (Kmax + 63) // 64
+    slot_x = np.zeros((E, nk * 64), dtype=F32)
+    slot_id = np.zeros((E, nk * 64), dtype=np.int64)
+    used = np.arange(nk * 64)[None, :] < K[:, None]
+    order = np.argsort(~cand, axis=1, kind="stable")[:, :nk * 64] if nk * 64 <= A else None
+    if order is None:
+        order = np.argsort(~cand, axis=1, kind="stable")
+        order = np.pad(order, ((0, 0), (0, nk * 64 - A)))
+    slot_id[:] = order
+    slot_x[:] = np.take_along_axis(X, np.minimum(order, A - 1), axis=1)
+    P = np.where(used, bk_expf(np.where(used, slot_x - m[:, None], F32(0))), F32(0)).astype(F32)
+    P = P.reshape(E, nk, 64)
+    s = np.zeros((E, 64), dtype=F32)
+    for k in range(nk):
+        s = s + P[:, k, :]  # unused slots add +0
+    incl = wave_scan_f32(s)
+    S = incl[:, 63].copy()
+    z = [mix64(int(st)) for st in rng]
+    new_rng = [(int(st) + GOLDEN) & M64 for st in rng]
+    u = np.array([zz >> 40 for zz in z], dtype=np.uint32).astype(F32) * F32(2.0 ** -24)
+    target = (S * u).astype(F32)
+    over = incl > target[:, None]
+    pos = s > F32(0)
+    last_pos = np.where(pos.any(1), 63 - pos[:, ::-1].argmax(1), 0)
+    sel = np.where(over.any(1), over.argmax(1), last_pos)
+    er = np.arange(E)
+    acc = np.where(sel > 0, incl[er, np.maximum(sel - 1, 0)], F32(0)).astype(F32)
+    pick = np.full(E, -1)
+    last = np.full(E, -1)
+    for k in range(nk):
+        pt = P[er, k, sel]
+        ok = (pt > F32(0)) & (pick < 0)
+        acc = np.where(ok, acc + pt, acc).astype(F32)
+        last = np.where(ok, 64 * k + sel, last)
+        pick = np.where(ok & (acc > target), 64 * k + sel, pick)
+    pick = np.where(pick < 0, last, pick)
+    good = pick >= 0
+    pk = np.maximum(pick, 0)
+    actions = np.where(good, slot_id[er, pk], A).astype(np.int32)
+    xa = slot_x[er, pk]
+    logp = np.where(good, xa - (m + bk_logf(np.maximum(S, F32(1)))), F32(np.nan)).astype(F32)
+    return actions, logp, new_rng
 
 
 def rng_index(state: int, K: int):
-    state = (state + 0x9E3779B97F4A7C15) & M64
+    state = (state + GOLDEN) & M64
     z = state
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
     z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
@@ -42,6 +169,13 @@ class VecEnvOracle:
 
     def mask(self, e):
         return self.o.legal_mask(self.states[e], 0)[0]
+
+    def sample_policy(self, logits, zero_masked: bool = True):
+        """The agent's moves from its policy logits [E, A] over each env's current legal mask
+        (k_vec_policy); advances each env's stream by one draw. -> (actions, logp)."""
+        masks = np.stack([self.mask(e) for e in range(self.E)])
+        act, logp, self.rng = policy_sample(logits, masks, self.rng, zero_masked)
+        return act, logp
 
     def step(self, e: int, action: int):
         s = self.states[e]

@@ -173,3 +173,44 @@ def test_ppo_trainer_updates_on_device_env(tmp_path):
     tr2 = PPOTrainer(hp)
     tr2._load_checkpoint(2)
     assert tr2.update == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_sampling", [True, False])
+def test_ppo_rollout_draws(device_sampling):
+    """The rollout's draw on the device (bk_vec_policy over the actor's raw logits) or through torch's
+    Categorical over FilterLegalMoves: the stored actions are the drawn ones and their log-probs are
+    finite and <= 0; a device draw is a legal id unless every legal logit of its row is exactly 0 —
+    the reference filter's all -1e9 row (ppo/agent.py:40-41), uniform over every id, which the
+    freshly initialised agent produces for a few envs whose last hidden layer is all zero."""
+    from blokus_rl_amd.ppo.trainer import PPOTrainer
+
+    hp = _hp(num_envs=64, num_steps=16, total_timesteps=64 * 16, agent_type="cnn", save_interval=10**6)
+    tr = PPOTrainer(hp, device_sampling=device_sampling)
+    obs, _ = tr.envs.reset(seed=0)
+    masks, acts, rows = [], [], []
+    orig_step, orig_sample = tr.envs.step, tr.envs.sample_policy
+
+    def rec_step(action):
+        masks.append(tr.envs.valid_mask().clone())
+        acts.append(action.long().clone())
+        return orig_step(action)
+
+    def rec_sample(logits, zero_masked=True):
+        rows.append(logits.clone())
+        return orig_sample(logits, zero_masked)
+
+    tr.envs.step, tr.envs.sample_policy = rec_step, rec_sample
+    tr._play_env(obs.float(), torch.zeros(64, device=tr.device))
+    assert len(acts) == hp.num_steps
+    illegal = 0
+    for t, (m, a) in enumerate(zip(masks, acts)):
+        assert torch.equal(tr.memory.actions[t].long(), a)
+        bad = ~m.gather(1, a.view(-1, 1)).view(-1)
+        if device_sampling:
+            no_candidate = ~(m & (rows[t] != 0)).any(dim=1)
+            assert bool((no_candidate | ~bad).all()), (t, torch.nonzero(bad & ~no_candidate).view(-1).tolist())
+        illegal += int(bad.sum())
+    lp = tr.memory.logprobs
+    assert bool(torch.isfinite(lp).all()) and bool((lp <= 0).all())
+    assert device_sampling or illegal <= 64  # torch's draw over the same filter (same quirk)

@@ -150,3 +150,129 @@ def test_ai_possible_indexes_and_masked_logits():
     logits = torch.randn(4, 919, device=env.device)
     ml = env.masked_logits(logits)
     assert bool((ml[~mask] == -1e9).all()) and torch.equal(ml[mask], logits[mask])
+
+
+# ------------------------------------------------------------------ the masked-policy draw
+def _policy_logits(E, A, t, rng):
+    """Seeded logits with the edge cases of FilterLegalMoves (ppo/agent.py:27-42): exact zeros
+    (+0 and -0) on ~1/8 of the ids, an all-zero row every 5th env (under zero_masked: no
+    candidate -> the reference's all -1e9 row, uniform over every id), and a large spread."""
+    x = (rng.standard_normal((E, A)) * (0.5 + 4.0 * (t % 3))).astype(np.float32)
+    x[rng.random((E, A)) < 0.125] = 0.0
+    x[rng.random((E, A)) < 0.02] = -0.0
+    x[::5] = 0.0
+    return x
+
+
+@pytest.mark.parametrize("max_cells,E", [(4, 37), (5, 32), (4, 8)])
+def test_policy_sample_matches_oracle(max_cells, E):
+    """bk_vec_policy vs oracle.vecenv_oracle.policy_sample every step of a rollout: actions,
+    log-probs and the env's random stream bitwise; zero_masked on and off; then the env steps
+    with the drawn actions (states, masks, rewards bitwise, as test_vector_env_matches_oracle)."""
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    env = BlokusVectorEnv(E, 7, max_cells)
+    ref = VecEnvOracle(E, 7, max_cells)
+    A = env.eng.A
+    env.reset(seed=2)
+    ref.reset(seed=2)
+    rng = np.random.default_rng(11)
+    uniform_rows = 0
+    for t in range(40):
+        zm = t % 4 != 3
+        x = _policy_logits(E, A, t, rng)
+        a, lp = env.sample_policy(torch.from_numpy(x).to(env.device), zero_masked=zm)
+        ra, rlp = ref.sample_policy(x, zero_masked=zm)
+        assert (a.cpu().numpy() == ra).all(), (t, np.nonzero(a.cpu().numpy() != ra)[0][:8])
+        assert (lp.cpu().numpy().view(np.uint32) == rlp.view(np.uint32)).all(), t
+        assert (env.rng.cpu().numpy().view(np.uint64) == np.array(ref.rng, dtype=np.uint64)).all(), t
+        if zm:
+            uniform_rows += int((rlp[::5] == 0.0).sum())
+        env.step_raw(a)
+        for e in range(E):
+            r, d = ref.step(e, int(ra[e]))
+            assert float(env.reward[e]) == r and int(env.done[e]) == d, (t, e)
+        _assert_env_equal(env, ref, t)
+    assert uniform_rows > 0  # the all -1e9 rows were drawn (log-prob 0, as torch gives them)
+
+
+def _policy_graph_rollout(E, steps_per_graph, replays, seed):
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    env = BlokusVectorEnv(E, 7, 4)
+    ref = VecEnvOracle(E, 7, 4)
+    env.reset(seed=seed)
+    ref.reset(seed=seed)
+    x = np.random.default_rng(seed).standard_normal((E, env.eng.A)).astype(np.float32) * 3.0
+    logits = torch.from_numpy(x).to(env.device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(steps_per_graph):
+            env.step_policy(logits)
+    torch.cuda.synchronize()
+    ended = 0
+    for r in range(replays):
+        g.replay()
+        torch.cuda.synchronize()
+        for _ in range(steps_per_graph):
+            ra, rlp = ref.sample_policy(x)
+            last = [ref.step(e, int(ra[e])) for e in range(E)]
+            ended += sum(d for _, d in last)
+        assert (env.actions.cpu().numpy() == ra).all(), r
+        assert (env.logp.cpu().numpy().view(np.uint32) == rlp.view(np.uint32)).all(), r
+        _assert_env_equal(env, ref, r)
+        assert env.reward.cpu().numpy().tolist() == [x_ for x_, _ in last], r
+    return ended
+
+
+def test_policy_rollout_benchmark_size_graph_matches_oracle():
+    """8192 envs (config 5) through the bench's path: a HIP graph of 5 x (bk_vec_policy +
+    k_vec_step7) replayed twice, checked against the oracle after each replay."""
+    assert _policy_graph_rollout(8192, 5, 2, seed=4) > 0
+
+
+def test_policy_rollout_ragged_size_graph_matches_oracle():
+    assert _policy_graph_rollout(8190, 3, 2, seed=6) > 0
+
+
+def test_policy_sample_law_and_logprob_vs_torch():
+    """The draw's law and log-probs against the reference's own ops: 8192 envs on the empty board
+    (the same legal set), one logits row: the action histogram vs softmax over the legal ids
+    (chi-square), log-probs vs Categorical(logits=FilterLegalMoves(x)).log_prob (the reference's
+    get_action_and_value, ppo/agent.py:148-156) at rtol 2e-6; with zero_masked, legal ids whose
+    logit is exactly 0 are never drawn, without it they are."""
+    from scipy import stats
+
+    from blokus_rl_amd.ppo.agent import FilterLegalMoves
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    E = 8192
+    env = BlokusVectorEnv(E, 7, 4)
+    env.reset(seed=0)
+    A = env.eng.A
+    g = torch.Generator().manual_seed(0)
+    row = torch.randn(A, generator=g) * 1.5
+    legal = env.valid_mask()[0].cpu()
+    lid = torch.nonzero(legal).view(-1)
+    row[lid[::4]] = 0.0  # every 4th legal id at exactly 0
+    x = row.repeat(E, 1).contiguous().to(env.device)
+    filt = FilterLegalMoves()(x, env.mask_words)
+    dist = torch.distributions.Categorical(logits=filt)
+    counts = torch.zeros(A, dtype=torch.int64)
+    for _ in range(8):  # 8 draws per env from the same state (the stream advances)
+        a, lp = env.sample_policy(x, zero_masked=True)
+        want = dist.log_prob(a.long())
+        torch.testing.assert_close(lp, want, rtol=2e-6, atol=2e-6)
+        counts += torch.bincount(a.long().cpu(), minlength=A)
+    probs = dist.probs[0].double().cpu()
+    assert int(counts[probs == 0].sum()) == 0  # illegal ids and the zero-logit legal ids
+    keep = probs > 0
+    exp = probs[keep] * counts.sum()
+    big = exp >= 5
+    chi = float((((counts[keep][big] - exp[big]) ** 2) / exp[big]).sum())
+    dof = int(big.sum()) - 1
+    assert stats.chi2.sf(chi, dof) > 1e-4, (chi, dof)
+    a, _ = env.sample_policy(x, zero_masked=False)
+    zero_ids = set(lid[::4].tolist())
+    hits = sum(1 for v in a.cpu().tolist() if v in zero_ids)
+    assert hits > 0

@@ -21,9 +21,13 @@ for d in dirs:
 means = {k: sum(v) / len(v) for k, v in acc.items()}
 fetch = 2 * means.get("FETCH_SIZE", 0.0) * 1024
 write = means.get("WRITE_SIZE", 0.0) * 1024
-doc = json.load(open(out)) if os.path.exists(out) else {"round": 1, "kernels": {}}
+rnd = int(os.environ.get("BK_PMC_ROUND", "6"))
+doc = json.load(open(out)) if os.path.exists(out) else {"round": rnd, "kernels": {}}
+doc["round"] = max(int(doc.get("round", rnd)), rnd)
 doc.setdefault("notes", {})[key] = note
 doc["kernels"][key] = {"units_per_launch": int(units), "hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch,
-                       "write_bytes": write, "algorithmic_bytes": int(float(algo)), "counters_per_dispatch": means}
+                       "write_bytes": write, "algorithmic_bytes": int(float(algo)), "dispatches": len(acc.get("FETCH_SIZE", [])),
+                       "kernel_pattern": pat, "counters_per_dispatch": means}
 json.dump(doc, open(out, "w"), indent=1)
-print(key, {k: round(v, 1) for k, v in doc["kernels"][key].items() if k != "counters_per_dispatch"})
+print(key, {k: (round(v, 1) if isinstance(v, float) else v) for k, v in doc["kernels"][key].items()
+           if k != "counters_per_dispatch"})
