@@ -178,6 +178,22 @@ def bench_dry(args, world, rank):
             "backend": dist.get_backend() if dist_active() else None}
 
 
+def _trace_avg_ms(csv_name: str, kernel_prefix: str):
+    """Average duration (ms) of the kernels named kernel_prefix* in a committed rocprofv3
+    --kernel-trace --stats summary (profiles/<csv_name>), or None."""
+    import csv
+
+    fp = os.path.join(ROOT, "profiles", csv_name)
+    if not os.path.exists(fp):
+        return None
+    with open(fp, newline="", encoding="utf-8") as f:
+        rows = [r for r in csv.DictReader(f) if r["Name"].startswith(kernel_prefix)]
+    if not rows:
+        return None
+    calls = sum(int(r["Calls"]) for r in rows)
+    return sum(float(r["TotalDurationNs"]) for r in rows) / calls / 1e6
+
+
 def _pmc_traffic(kernel_prefix: str, units_per_launch: int, with_source: bool = False):
     """HBM bytes per launch from the committed rocprofv3 PMC summaries (profiles/*pmc*.json) of this
     kernel at this launch size, FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md
@@ -708,18 +724,28 @@ def bench_train(args, world, rank):
     return out
 
 
+MFMA_F32_PEAK = 157.3e12  # FLOP/s, f32-input MFMA = the f32 vector peak (MI355X_MICROARCH.md chip table)
+
+
 def bench_ppo(args, world, rank):
     """§8f row 4: whole PPO updates on the config-5 device env (reference config
-    ppo_blokus_7x7.yml: cnn agent, d_model 128, 32 steps per rollout; 8192 envs per GPU):
-    rollout (fused env step + device legal filter) + GAE kernel + 4 epochs of minibatch updates."""
-    from blokus_rl_amd.ppo.trainer import PPOHparams, PPOTrainer
+    ppo_blokus_7x7.yml: cnn agent, d_model 128, 32 steps per rollout; 8192 envs per GPU): each
+    update = the rollout (agent forward + bk_vec_policy + k_vec_step7 per step, ppo/trainer.py:128-175)
+    + the GAE kernel (:177-211) + 4 epochs x 4 minibatches of the clipped update (:213-311).
+    The agent's convolutions run on MIOpen (NCHW, fp32); the bench sets MIOPEN_FIND_MODE=FAST in its
+    own process (`ppo_update_subprocess`): the default find mode spends ~160 s building kernels on a
+    fresh box for the same steady-state update time (round 6: 157.5 s vs 4.5 s warm-up, 2.00 vs 2.03 s
+    per update)."""
+    from blokus_rl_amd.ppo.trainer import PPOHparams, PPOTrainer, compute_gae
 
     E, T = args.envs, 32
     hp = PPOHparams(num_envs=E, num_steps=T, agent_type="cnn", d_model=128, learning_rate=1e-5,
                     total_timesteps=E * T * 100, seed=rank, save_interval=10**9, target_kl=None)
     tr = PPOTrainer(hp)
-    tr.train(1)  # warm-up update
+    tw = time.perf_counter()
+    tr.train(1)  # warm-up update (MIOpen's first-use kernel builds for the agent's convs land here)
     torch.cuda.synchronize()
+    warm_s = time.perf_counter() - tw
     _barrier(world)
     t0 = time.perf_counter()
     n = args.ppo_updates
@@ -727,12 +753,37 @@ def bench_ppo(args, world, rank):
     torch.cuda.synchronize()
     _barrier(world)
     dt = _max_over_ranks(time.perf_counter() - t0, world)
-    # the GAE kernel alone on this rollout
-    from blokus_rl_amd.ppo.trainer import compute_gae
-    m = tr.memory
-    nv = torch.zeros(E, device=tr.device)
+    # where an update's time goes (one more update with synchronizing phase timers; not in value)
+    tr.phase_timers = True
+    tr.train(1)
+    phases = dict(tr.phase_s)
+    dev = tr.device
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the update's dominant kernel: the 128 -> 128 3x3 conv's input gradient at the minibatch size
+    # (MIOpen igemm_bwd_gtcx35_nhwc fp32 on the f32 matrix cores, behind its NCHW -> NHWC transposes;
+    # r06 kernel trace: profiles/r06_ppo_kernel_stats.csv), timed alone with events on the stream it
+    # runs on (the event pair also holds the transposes)
+    mb = hp.minibatch_size
+    conv = tr.agent.conv_block.conv_block[3]
+    xg = torch.randn((mb, hp.d_model, 7, 7), device=dev)
+    xg.requires_grad_(True)
+    yg = conv(xg)
+    dyg = torch.randn_like(yg)
+    for _ in range(2):
+        torch.autograd.grad(yg, xg, dyg, retain_graph=True)
+    torch.cuda.synchronize()
+    e0.record(st)
+    for _ in range(5):
+        torch.autograd.grad(yg, xg, dyg, retain_graph=True)
+    e1.record(st)
+    torch.cuda.synchronize()
+    dgrad_ms = e0.elapsed_time(e1) / 5
+    conv_flop = 2.0 * mb * 49 * hp.d_model * hp.d_model * 9
+    del xg, yg, dyg
+    # the GAE kernel alone on this rollout
+    m = tr.memory
+    nv = torch.zeros(E, device=dev)
     compute_gae(m.rewards, m.values, m.dones, nv, nv, 0.99, 0.95)
     e0.record(st)
     for _ in range(20):
@@ -741,10 +792,106 @@ def bench_ppo(args, world, rank):
     torch.cuda.synchronize()
     gae_ms = e0.elapsed_time(e1) / 20
     gae_bytes = 5 * T * E * 4 + 2 * E * 4
-    return {"metric": "PPO env-steps/sec incl. updates (7x7 cnn agent, 32-step rollouts)",
-            "value": E * T * n * world / dt, "unit": "env-steps/s", "envs_per_gpu": E, "updates": n,
-            "s_per_update": dt / n, "last_log": {k: float(v) for k, v in tr.logs[-1].items()},
-            "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBps": gae_bytes / (gae_ms * 1e-3) / 1e9}}
+    out = {"metric": "PPO env-steps/sec incl. updates (7x7 cnn agent d_model 128, 32-step rollouts, 4 x 4 minibatches)",
+           "value": E * T * n * world / dt, "unit": "env-steps/s", "envs_per_gpu": E, "updates": n,
+           "updates_per_s": n / dt, "s_per_update": dt / n, "warmup_update_s": warm_s,
+           "miopen_find_mode": os.environ.get("MIOPEN_FIND_MODE"), "dtype": "fp32",
+           "phase_s_one_update": phases,
+           "last_log": {k: float(v) for k, v in tr.logs[-1].items()},
+           "roofline": {"bound": "mfma", "kernel": "MIOpen igemm_bwd (conv 128->128 3x3 input gradient, fp32, with its NCHW<->NHWC transposes)",
+                        "achieved": conv_flop / (dgrad_ms * 1e-3) / 1e12, "peak": MFMA_F32_PEAK / 1e12,
+                        "unit": "TFLOP/s", "frac": conv_flop / (dgrad_ms * 1e-3) / MFMA_F32_PEAK, "kernel_ms": dgrad_ms,
+                        "flop_per_launch": conv_flop, "units_per_launch": mb, "traffic": None,
+                        "kernel_only_ms_trace": _trace_avg_ms("r06_ppo_kernel_stats.csv", "igemm_bwd_gtcx35_nhwc_fp32"),
+                        "kernel_only_trace_source": "r06_ppo_kernel_stats.csv",
+                        "note": "one of the update's three equal-cost conv kernels (fwd / dgrad / wgrad, ~17% of the "
+                                "update's GPU time each in the kernel trace); f32-input MFMA peak 157.3 TF"},
+           "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBps": gae_bytes / (gae_ms * 1e-3) / 1e9}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_ppo(hp)
+    return out
+
+
+def cpu_baseline_ppo(hp_gpu):
+    """The reference's PPO iteration on the host cores at a bounded size: 64 envs of the CPU
+    restatement (oracle/vecenv_oracle.py, a Python loop per env like SyncVectorEnv), the same cnn
+    agent on the CPU (torch, all granted threads), FilterLegalMoves + Categorical per step
+    (ppo/agent.py:27-42, 148-156), GAE (oracle/ppo_oracle.py) and one optimize_agent pass (4 epochs
+    x 4 minibatches of 512): one whole update, timed."""
+    import dataclasses
+
+    from blokus_rl_amd.ppo.agent import get_agent
+    from blokus_rl_amd.ppo.trainer import optimize_agent
+    from oracle.ppo_oracle import filter_legal, gae_f32
+    from oracle.vecenv_oracle import VecEnvOracle
+
+    threads = cpu_workers()
+    old_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        E, T = 64, hp_gpu.num_steps
+        hp = dataclasses.replace(hp_gpu, num_envs=E)
+        torch.manual_seed(0)
+        agent = get_agent("cnn")((7, 7), 919, hp)
+        opt = torch.optim.Adam(agent.parameters(), lr=hp.learning_rate, eps=hp.eps)
+        env = VecEnvOracle(E, 7, 4)
+        env.reset(0)
+        obs = torch.zeros((T, E, 7, 7))
+        acts, lps, vals, rews, dones = (torch.zeros((T, E)) for _ in range(5))
+        t0 = time.perf_counter()
+        nobs = torch.from_numpy(np.stack([env.obs(e) for e in range(E)])).float()
+        ndone = torch.zeros(E)
+        for t in range(T):
+            obs[t], dones[t] = nobs, ndone
+            with torch.inference_mode():
+                h = agent.features(nobs)
+                mask = np.zeros((E, 919), np.float32)
+                for e in range(E):
+                    m = env.mask(e)
+                    mask[e] = np.unpackbits(m.view(np.uint8), bitorder="little")[:919]
+                logits = torch.from_numpy(filter_legal(agent.actor(h).numpy(), mask))
+                dist = torch.distributions.Categorical(logits=logits)
+                a = dist.sample()
+                lps[t], vals[t], acts[t] = dist.log_prob(a), agent.critic(h).view(-1), a.float()
+            res = [env.step(e, int(a[e])) for e in range(E)]
+            rews[t] = torch.tensor([r for r, _ in res])
+            ndone = torch.tensor([float(d) for _, d in res])
+            nobs = torch.from_numpy(np.stack([env.obs(e) for e in range(E)])).float()
+        with torch.inference_mode():
+            nv = agent.get_value(nobs).view(-1).numpy()
+        adv, ret = gae_f32(rews.numpy(), vals.numpy(), dones.numpy(), nv, ndone.numpy(), hp.gamma, hp.gae_lambda)
+        batch = {"obs": obs.reshape(-1, 7, 7), "logprobs": lps.reshape(-1), "actions": acts.reshape(-1),
+                 "advantages": torch.from_numpy(adv).reshape(-1), "returns": torch.from_numpy(ret).reshape(-1),
+                 "values": vals.reshape(-1)}
+        t1 = time.perf_counter()
+        optimize_agent(agent, opt, batch, hp)
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(old_threads)
+    return {"value": E * T / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"one whole PPO update at 64 envs x {T} steps (rollout {t1 - t0:.1f} s: C-oracle envs in a Python "
+                      f"loop + the cnn agent on {threads} CPU threads; update {dt - (t1 - t0):.1f} s: 4 epochs x 4 "
+                      f"minibatches of 512) in {dt:.1f} s"}
+
+
+def ppo_update_subprocess(args):
+    """The PPO leg of the default run in a child process of its own (MIOPEN_FIND_MODE=FAST there
+    only, so MIOpen's other users in this process keep the default mode); its JSON line back."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "ppo", "--ppo-updates", str(args.ppo_updates),
+           "--envs", str(args.envs)] + (["--no-cpu-baseline"] if args.no_cpu_baseline else [])
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                            "MASTER_PORT", "BK_DIST_BACKEND")}
+    env["MIOPEN_FIND_MODE"] = "FAST"
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.ppo_timeout, check=False)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-800:]}
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {args.ppo_timeout} s"}
 
 
 def main():
@@ -755,6 +902,7 @@ def main():
     ap.add_argument("--workload", choices=["all", "legal", "selfplay", "vecenv", "train", "ppo", "dry"],
                     default="all")
     ap.add_argument("--ppo-updates", type=int, default=2)
+    ap.add_argument("--ppo-timeout", type=float, default=240.0)
     ap.add_argument("--train-batch", type=int, default=1024)
     ap.add_argument("--train-steps", type=int, default=20)
     ap.add_argument("--train-rows", type=int, default=8192)
@@ -854,6 +1002,7 @@ def main():
             out["learner"] = bench_train(args, world, rank)
             if world == 1:
                 out["config1_7x7"] = bench_config1(args, args.cpu_pool, args.cpu_workers)
+                out["ppo_update"] = ppo_update_subprocess(args)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             pool, nw = args.cpu_pool, args.cpu_workers
             out["cpu_baseline"] = cpu_baseline_selfplay(args.cpu_seconds, args.model, pool, nw)

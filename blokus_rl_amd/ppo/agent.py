@@ -122,7 +122,7 @@ class CnnAgent(_ActorCritic):
 
     def features(self, x):
         h = self.conv_block(x)
-        return h.view(h.size(0), -1)
+        return h.reshape(h.size(0), -1)  # (c, h, w) order whatever the conv layout (channels_last too)
 
 
 class MlpAgent(_ActorCritic):
