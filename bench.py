@@ -29,6 +29,7 @@ from blokus_rl_amd.replay import dist_active  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
 MFMA_F16_PEAK = 2.5e15  # FLOP/s, dense f16 MFMA (MI355X_MICROARCH.md; not the 2:1-sparsity figure)
+MFMA_F32_PEAK = 157.3e12  # FLOP/s, f32-input MFMA = the f32 vector peak (MI355X_MICROARCH.md chip table)
 
 # Algorithmic bytes of one board in k_legal_mask: the packed state read (384 B) + the
 # 30433-bit mask written (476 u64 = 3808 B) + its count (4 B). DESIGN.md §4.
@@ -192,6 +193,24 @@ def _trace_avg_ms(csv_name: str, kernel_prefix: str):
         return None
     calls = sum(int(r["Calls"]) for r in rows)
     return sum(float(r["TotalDurationNs"]) for r in rows) / calls / 1e6
+
+
+def _window_trace(kernel: str, args):
+    """The committed kernel-trace window averages (profiles/r06_window_trace.json, tools/window_avg.py)
+    when they were taken with this run's warmup / steps / sims / games, else None."""
+    fp = os.path.join(ROOT, "profiles", "r06_window_trace.json")
+    try:
+        with open(fp, encoding="utf-8") as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if (d.get("warmup"), d.get("steps"), d.get("sims"), d.get("games", args.games)) != (args.warmup, args.steps,
+                                                                                          args.sims, args.games):
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    if not k or not k.get("window_avg_us"):
+        return None
+    return dict(k, source=os.path.basename(fp))
 
 
 def _pmc_traffic(kernel_prefix: str, units_per_launch: int, with_source: bool = False):
@@ -702,29 +721,40 @@ def bench_train(args, world, rank):
            "config": {"workload": "§8f row 1 learner", "batch_per_gpu": args.train_batch,
                       "global_batch": args.train_batch * world, "parallelism": f"ddp{world}"},
            "device_path": main_r["device_path"],
-           "path": ("tower convs (forward + input gradient) on bk_conv_x3 (split-f16 MFMA, fp32-class), "
-                    "channels_last, PyTorch batch norm" if main_r["device_path"] else "fp32 MIOpen"),
+           "path": ("tower convs on trainconv.hip (forward + input gradient: k_conv_x3; weight gradient: "
+                    "k_conv_x3_wgrad; split-f16 MFMA, fp32-class), the 64-channel train-mode batch norms on "
+                    "trainbn.hip (k_bn_reduce / k_bn_axpb), channels_last; stem, heads and Adam on PyTorch"
+                    if main_r["device_path"] else "fp32 MIOpen"),
            "fp32_miopen_same_batch": {k: res["fp32"][k] for k in ("value", "unit", "ms_per_step")},
            "at_reference_batch_64": {k: res["b64"][k] for k in ("value", "unit", "ms_per_step", "device_path")},
            "roofline": {"bound": "hbm", "kernel": lk["kernel"], "achieved": lk["achieved_GBps"],
                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk["achieved_GBps"] * 1e9 / HBM_PEAK,
                         "kernel_ms": lk["ms"], "bytes_per_launch_pair": lk["bytes_per_launch_pair"],
-                        "units_per_launch": args.train_batch, "traffic": None}}
+                        "units_per_launch": args.train_batch,
+                        "traffic": _pmc_traffic("k_policy_loss+grad", args.train_batch)}}
     if "conv_kernel" in main_r:  # the device path's dominant kernel: k_conv_x3 on the f16 matrix cores
         ck = main_r["conv_kernel"]
         out["loss_roofline"] = out["roofline"]
         out["roofline"] = {"bound": "mfma", "kernel": ck["kernel"], "achieved": ck["flop"] / (ck["ms"] * 1e-3) / 1e12,
                            "peak": MFMA_F16_PEAK / 1e12, "unit": "TFLOP/s",
                            "frac": ck["flop"] / (ck["ms"] * 1e-3) / MFMA_F16_PEAK, "kernel_ms": ck["ms"],
-                           "flop_per_launch": ck["flop"], "units_per_launch": args.train_batch, "traffic": None,
+                           "flop_per_launch": ck["flop"], "units_per_launch": args.train_batch,
+                           "traffic": _pmc_traffic("k_conv_x3", args.train_batch),
                            "fp32_equiv_tflops": ck["fp32_equiv_flop"] / (ck["ms"] * 1e-3) / 1e12,
-                           "note": "executed split-f16 MFMA work (3 f16 products per fp32 product)"}
+                           "frac_algorithmic": ck["fp32_equiv_flop"] / (ck["ms"] * 1e-3) / MFMA_F16_PEAK,
+                           "note": "frac: executed split-f16 MFMA work (3 f16 products per fp32 product); "
+                                   "frac_algorithmic: the fp32 conv's FLOP"}
+        if "wgrad_kernel" in main_r:
+            wk = main_r["wgrad_kernel"]
+            out["wgrad_roofline"] = {"bound": "mfma", "kernel": wk["kernel"], "kernel_ms": wk["ms"],
+                                     "achieved": wk["flop"] / (wk["ms"] * 1e-3) / 1e12, "peak": MFMA_F16_PEAK / 1e12,
+                                     "unit": "TFLOP/s", "frac": wk["flop"] / (wk["ms"] * 1e-3) / MFMA_F16_PEAK,
+                                     "frac_algorithmic": wk["fp32_equiv_flop"] / (wk["ms"] * 1e-3) / MFMA_F16_PEAK,
+                                     "flop_per_launch": wk["flop"], "units_per_launch": args.train_batch,
+                                     "traffic": _pmc_traffic("k_conv_x3_wgrad", args.train_batch)}
     if "reference_path" in res["b64"]:
         out["reference_path_batch_64"] = res["b64"]["reference_path"]
     return out
-
-
-MFMA_F32_PEAK = 157.3e12  # FLOP/s, f32-input MFMA = the f32 vector peak (MI355X_MICROARCH.md chip table)
 
 
 def bench_ppo(args, world, rank):
@@ -958,14 +988,25 @@ def main():
         out = bench_selfplay(args, world, rank)
         sr = out.get("search_roofline", {})
         if "k_leaf_step" in sr.get("kernel", ""):
-            # HBM-side bytes per launch of the search kernel (profiles/*pmc*leafstep*.json) over its
-            # live launch time: the fraction of the HBM roofline it actually draws
-            # (a committed profile's bytes over this run's time: an estimate, named as one)
+            # the leaf step's time over the timed window: the average over the window's launches in
+            # the committed kernel trace of this same command (profiles/r06_window_trace.json,
+            # tools/window_avg.py), beside this run's live sample after the window; HBM-side bytes
+            # per launch from the committed PMC passes over the same window: the fraction of the
+            # HBM roofline it draws (committed profiles, named as such)
+            sr["k_leaf_step_us_live_after_window"] = sr.pop("k_leaf_step_us", None)
+            win = _window_trace("k_leaf_step_ov", args)
+            sr["k_leaf_step_us"] = win["window_avg_us"] if win else sr["k_leaf_step_us_live_after_window"]
+            sr["k_leaf_step_us_source"] = (f"kernel-trace average over the window's {win['window_dispatches']} "
+                                           f"launches, {win['source']}" if win else "live sample after the window")
             tr, src = _pmc_traffic("k_leaf_step_ov", args.games, with_source=True)
             sr["traffic"], sr["traffic_source"] = tr, src
             if tr and sr.get("k_leaf_step_us"):
                 sr["achieved_est"] = tr / (sr["k_leaf_step_us"] * 1e-6) / 1e9
                 sr["frac_est"] = sr["achieved_est"] / sr["peak"]
+        tw = _window_trace("k_leafnet_x3", args)
+        if tw and "tower_roofline" in out:
+            out["tower_roofline"]["kernel_ms_window_trace"] = tw["window_avg_us"] / 1e3
+            out["tower_roofline"]["kernel_ms_window_trace_source"] = tw["source"]
         kname = out["roofline"].get("kernel", "").split(" ")[0]
         if kname.startswith("k_conv3x3") or kname.startswith("k_tower") or kname.startswith("k_leafnet"):
             # HBM bytes per launch from the committed PMC passes (profiles/r01_pmc_conv*.json)

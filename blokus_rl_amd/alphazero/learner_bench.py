@@ -93,6 +93,28 @@ def time_conv_x3(batch: int, device, reps: int = 20) -> dict:
             "fp32_equiv_flop": 2.0 * batch * 400 * 64 * 576}
 
 
+def time_conv_x3_wgrad(batch: int, device, reps: int = 20) -> dict:
+    """bk_conv_x3_wgrad (k_conv_x3_wgrad + its fixed-order reduce) alone at the learner's batch: its
+    executed MFMA work per launch = batch x 8 waves x 15 K-chunks (24-wide rows: 480 of 400 pixels)
+    x 54 v_mfma_f32_16x16x32_f16; the fp32-equivalent = 2 x batch x 400 x 64 x 576."""
+    from .train_conv import conv_x3_wgrad
+
+    g = torch.Generator(device=device).manual_seed(1)
+    x = torch.randn(batch, 64, 20, 20, device=device, generator=g).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(batch, 64, 20, 20, device=device, generator=g).contiguous(memory_format=torch.channels_last)
+    for _ in range(3):
+        conv_x3_wgrad(x, gy)
+    st = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        conv_x3_wgrad(x, gy)
+    e1.record(st)
+    torch.cuda.synchronize()
+    return {"kernel": "k_conv_x3_wgrad + k_conv_x3_wgrad_reduce", "ms": e0.elapsed_time(e1) / reps,
+            "flop": float(batch) * 8 * 15 * 54 * 16384, "fp32_equiv_flop": 2.0 * batch * 400 * 64 * 576}
+
+
 def reference_loop_loss(masks, p_pred, v_pred, p_gt, v_gt):
     """compute_loss as written in neural_network.py:138-157 (per-sample loop)."""
     v_loss = (v_pred.squeeze() - v_gt).pow(2).mean()
@@ -182,6 +204,7 @@ def bench_learner(eng, world: int, rank: int, batch: int, steps: int, warmup: in
                             "bytes_per_launch_pair": kbytes, "achieved_GBps": kbytes / (kms * 1e-3) / 1e9}}
     if L.device_path:
         out["conv_kernel"] = time_conv_x3(batch, eng.device)
+        out["wgrad_kernel"] = time_conv_x3_wgrad(batch, eng.device)
     if reference_steps and rank == 0 and world == 1:
         ref_model = ResNet(eng.N, eng.P, eng.A, 5).to(eng.device)
         out["reference_path"] = bench_reference_path(eng, states, ids, pi, k, z, batch, reference_steps, ref_model)

@@ -320,6 +320,13 @@ def bench_selfplay(args, world, rank):
                            "achieved": cflop / (cms * 1e-3) / 1e12, "peak": cpeak / 1e12, "unit": "TFLOP/s",
                            "frac": cflop / (cms * 1e-3) / cpeak, "traffic": None, "kernel_ms": cms,
                            "flop_per_launch": cflop, "units_per_launch": G,
+                           # the leaf's algorithmic work = the direct conv + heads
+                           # arithmetic of the fp32 network (298.6 MFLOP per 20x20 leaf), whatever the
+                           # kernel executes (x3: 3 f16 products per fp32 product)
+                           "algorithmic_flop_per_launch": dflop,
+                           "frac_algorithmic": dflop / (cms * 1e-3) / cpeak,
+                           "frac_note": "frac = executed MFMA work / peak (3 f16 products per fp32 product on x3); "
+                                        "frac_algorithmic = the fp32 network's conv FLOP / peak",
                            "direct_conv_equiv_tflops": dflop / (cms * 1e-3) / 1e12,
                            "launches_per_sim_step": conv["launches"],
                            "share_of_sim_step": conv["launches"] * cms / (elapsed / steps_sim * 1e3)}
