@@ -1,10 +1,17 @@
 #!/bin/bash
-# Full default bench (as the driver runs it) + selfplay GPU tests.
+# The bench as the driver runs it (N=1), optionally followed by the same command under
+# rocprofv3 --kernel-trace --stats (PROFILE=1; the stats CSV -> gpurun_out/bench_kernel_stats.csv).
+#   tools/gpu/bench.sh [steps] [warmup]
 cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests/test_selfplay_gpu.py -x -q -p no:cacheprovider > gpurun_out/pytest_sp.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_sp.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py > gpurun_out/bench_all.json 2> gpurun_out/bench_all.err
-rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_all.json; grep -v amdgpu.ids gpurun_out/bench_all.err | tail -5
-exit $rc
+S=${1:-20} W=${2:-5}
+timeout -k 10 420 python bench.py --gpus 1 --steps $S --warmup $W > gpurun_out/bench.json 2> gpurun_out/bench.err \
+  || { tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+if [ "${PROFILE:-0}" = "1" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/bench_kt -o kt --output-format csv -- python bench.py --gpus 1 --steps $S --warmup $W \
+    > gpurun_out/bench_kt.json 2> gpurun_out/bench_kt.err || { tail -20 gpurun_out/bench_kt.err; exit 1; }
+  for f in $(find /tmp/bench_kt -name "*kernel_stats.csv"); do grep -q k_leaf_step_ov $f && cp $f gpurun_out/bench_kernel_stats.csv; done
+  head -12 gpurun_out/bench_kernel_stats.csv | cut -c1-160
+fi
