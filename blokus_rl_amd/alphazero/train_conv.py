@@ -81,6 +81,7 @@ class ConvX3Function(torch.autograd.Function):
         return y
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
@@ -115,6 +116,7 @@ class BatchNormFunction(torch.autograd.Function):
         return y
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, gy):
         lib = load_library()
         x, weight, stats = ctx.saved_tensors
@@ -163,11 +165,13 @@ def _eligible(m: nn.Module) -> bool:
 
 
 class X3Conv2d(nn.Conv2d):
-    """nn.Conv2d (same parameters and state_dict keys) whose 20x20 64->64 device calls run
-    ConvX3Function; anything else (CPU, other shapes) takes nn.Conv2d's own path."""
+    """nn.Conv2d (same parameters and state_dict keys) whose 20x20 64->64 device calls in training
+    (train mode, gradients enabled) run ConvX3Function; anything else (eval mode, no_grad /
+    inference, CPU, other shapes) takes nn.Conv2d's own fp32 path."""
 
     def forward(self, x):
-        if x.is_cuda and x.dim() == 4 and tuple(x.shape[1:]) == (64, 20, 20) and x.dtype == torch.float32:
+        if (self.training and torch.is_grad_enabled() and x.is_cuda and x.dim() == 4
+                and tuple(x.shape[1:]) == (64, 20, 20) and x.dtype == torch.float32):
             return ConvX3Function.apply(x, self.weight, self.bias)
         return super().forward(x)
 
@@ -184,9 +188,11 @@ def use_x3_convs(model: nn.Module) -> int:
 
 
 def prepare_model(model: nn.Module, x3_convs: bool = True, fused_bn: bool = True) -> nn.Module:
-    """The device training path in place: channels_last parameters, PyTorch batch norm (the
-    64-channel ones on bk_bn_forward / bk_bn_backward when fused_bn), and (x3_convs) the tower
-    convs on bk_conv_x3."""
+    """The device training path IN PLACE on the caller's model (Learner(device_path="auto") calls
+    it): channels_last parameters, PyTorch batch norm (the 64-channel ones on bk_bn_forward /
+    bk_bn_backward when fused_bn), and (x3_convs) the tower convs on bk_conv_x3. The swapped
+    classes keep the parameters and state_dict keys; their eval-mode and no-grad forwards are
+    PyTorch's fp32 ones, so a deepcopy of the model (e.g. the trainer's pnet) evaluates in fp32."""
     use_native_batchnorm(model)
     if fused_bn:
         use_fused_batchnorm(model)

@@ -20,15 +20,21 @@ from torch import nn
 
 class NativeBatchNorm2d(nn.BatchNorm2d):
     """nn.BatchNorm2d on PyTorch's own batch-norm kernels instead of MIOpen's (same parameters,
-    buffers and state_dict keys; training-mode batch statistics and running-stat updates alike)."""
+    buffers and state_dict keys; training-mode batch statistics and running-stat updates alike):
+    nn.BatchNorm2d.forward's bookkeeping, then aten::native_batch_norm directly (F.batch_norm would
+    pick MIOpen; switching the process-wide cudnn flag around it is not thread-safe)."""
 
     def forward(self, x):
-        prev = torch._C._get_cudnn_enabled()
-        torch._C._set_cudnn_enabled(False)  # F.batch_norm reads the flag; the backward follows the forward
-        try:
-            return super().forward(x)
-        finally:
-            torch._C._set_cudnn_enabled(prev)
+        self._check_input_dim(x)
+        factor = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            factor = 1.0 / float(self.num_batches_tracked) if self.momentum is None else self.momentum
+        use_batch = self.training or (self.running_mean is None and self.running_var is None)
+        track = not self.training or self.track_running_stats
+        rm = self.running_mean if track else None
+        rv = self.running_var if track else None
+        return torch.native_batch_norm(x, self.weight, self.bias, rm, rv, use_batch, factor, self.eps)[0]
 
 
 def use_native_batchnorm(model: nn.Module) -> nn.Module:
@@ -380,9 +386,6 @@ def leafnet_x3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
     return (pf, v, out) if want_out else (pf, v)
 
 
-_W3_WS: dict = {}
-
-
 def leafnet_w3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
     """bk_leafnet_w3: leafnet_x3's network and outputs with the residual tower as Winograd
     F(2x2,3x3) convolutions on split-f16 products (20x20 boards)."""
@@ -399,11 +402,13 @@ def leafnet_w3(obs: torch.Tensor, model: "LeafResNet", want_out: bool = False):
     v = torch.empty((B, P), dtype=torch.float32, device=obs.device)
     out = torch.empty((B, 64, N, N), dtype=torch.float32, device=obs.device,
                       memory_format=torch.channels_last) if want_out else None
-    # the stem output's workspace, kept per device and batch (a captured graph reuses the pointer)
-    key = (obs.device, B, N)
-    ws = _W3_WS.get(key)
+    # the stem output's workspace, kept per model instance, device, batch and stream (a captured graph
+    # reuses the pointer; two evaluators or streams never share one)
+    cache = model.__dict__.setdefault("_w3_ws", {})
+    key = (obs.device, B, N, torch.cuda.current_stream(obs.device).cuda_stream)
+    ws = cache.get(key)
     if ws is None:
-        ws = _W3_WS[key] = torch.empty((B, N * N, 64), dtype=torch.float32, device=obs.device)
+        ws = cache[key] = torch.empty((B, N * N, 64), dtype=torch.float32, device=obs.device)
     h = model.x3_heads
     _check(lib.bk_leafnet_w3(
         ctypes.c_void_p(obs.data_ptr()), B, N, cin, _ptr(model.x3_wstem), _ptr(model.x3_sstem), _ptr(h[0]), nl,

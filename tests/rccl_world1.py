@@ -30,6 +30,10 @@ def main():
     from blokus_rl_amd.engine import Engine
     from blokus_rl_amd.nets import ResNet
 
+    # deterministic MIOpen backward (no atomic-order rounding): at world size 1 the DDP all-reduce
+    # must then leave the gradients bit-identical to the plain backward's
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
@@ -76,8 +80,7 @@ def main():
     opt.step()
     torch.cuda.synchronize()
     out["loss_ddp"], out["loss_plain"] = float(loss_a), float(loss_b)
-    # gradients: the DDP all-reduce at world size 1 must leave them as the plain backward's, up to
-    # the run-to-run rounding of the training-mode conv backward (MIOpen)
+    # gradients: the DDP all-reduce at world size 1 must leave them as the plain backward's
     out["grad_max_rel_diff"] = max(float((ga - gb).abs().max()) / (float(gb.abs().max()) + 1e-30)
                                    for ga, gb in zip(grads_a, grads_b))
     diff = 0.0
