@@ -17,7 +17,9 @@ import torch
 from torch import nn
 
 from ..engine import _check, _ptr, _stream, load_library
-from ..nets import NativeBatchNorm2d, use_native_batchnorm
+import torch.nn.functional as F
+
+from ..nets import NativeBatchNorm2d, ResNet, use_native_batchnorm
 
 
 def pack_weight(weight: torch.Tensor, flip: bool) -> tuple[torch.Tensor, torch.Tensor]:
@@ -96,41 +98,92 @@ class ConvX3Function(torch.autograd.Function):
         return gx, gw, gb
 
 
+def bn_forward(x: torch.Tensor, gamma, beta, rmean, rvar, momentum: float, eps: float, relu: bool):
+    """bk_bn_forward_ex on a channels_last [B, 64, H, W] f32 activation -> (y, stats [256])."""
+    lib = load_library()
+    M = x.numel() // 64
+    ws = torch.empty(lib.bk_bn_workspace_doubles(), dtype=torch.float64, device=x.device)
+    stats = torch.empty(256, dtype=torch.float32, device=x.device)
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    _check(lib.bk_bn_forward_ex(ctypes.c_void_p(x.data_ptr()), M, _ptr(gamma), _ptr(beta), _ptr(rmean), _ptr(rvar),
+                                float(momentum), float(eps), _ptr(ws), _ptr(stats), ctypes.c_void_p(y.data_ptr()),
+                                int(relu), _stream(x.device)))
+    return y, stats
+
+
+def bn_backward(gy: torch.Tensor, x: torch.Tensor, gamma, stats, relu: bool, want_dsum: bool):
+    """bk_bn_backward_ex -> (dx, dgamma, dbeta, dsum or None); dsum = the column sums of dx (the bias
+    gradient of the conv that produced x)."""
+    lib = load_library()
+    M = x.numel() // 64
+    ws = torch.empty(lib.bk_bn_workspace_doubles(), dtype=torch.float64, device=x.device)
+    ws2 = torch.empty(lib.bk_bn_workspace2_doubles(), dtype=torch.float64, device=x.device) if want_dsum else None
+    coef = torch.empty(256, dtype=torch.float32, device=x.device)
+    dg = torch.empty(64, dtype=torch.float32, device=x.device)
+    db = torch.empty(64, dtype=torch.float32, device=x.device)
+    ds = torch.empty(64, dtype=torch.float32, device=x.device) if want_dsum else None
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    _check(lib.bk_bn_backward_ex(ctypes.c_void_p(gy.data_ptr()), ctypes.c_void_p(x.data_ptr()), M, _ptr(gamma),
+                                 _ptr(stats), _ptr(ws), _ptr(coef), _ptr(dg), _ptr(db), ctypes.c_void_p(dx.data_ptr()),
+                                 int(relu), _ptr(ds), _ptr(ws2), _stream(x.device)))
+    return dx, dg, db, ds
+
+
 class BatchNormFunction(torch.autograd.Function):
-    """Train-mode batch norm of a channels_last [B, 64, H, W] f32 activation on bk_bn_forward /
-    bk_bn_backward (fp64 statistics, one streaming read per reduction); updates the running
-    statistics in place like nn.BatchNorm2d."""
+    """Train-mode batch norm (+ the following ReLU when relu) of a channels_last [B, 64, H, W] f32
+    activation on bk_bn_forward_ex / bk_bn_backward_ex (fp64 statistics, one streaming read per
+    reduction; the ReLU's mask recomputed from x in the backward, no extra pass); updates the
+    running statistics in place like nn.BatchNorm2d."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
-        lib = load_library()
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu):
         x = x.contiguous(memory_format=torch.channels_last)
-        M = x.numel() // 64
-        ws = torch.empty(lib.bk_bn_workspace_doubles(), dtype=torch.float64, device=x.device)
-        stats = torch.empty(256, dtype=torch.float32, device=x.device)
-        y = torch.empty_like(x, memory_format=torch.channels_last)
-        _check(lib.bk_bn_forward(ctypes.c_void_p(x.data_ptr()), M, _ptr(weight), _ptr(bias), _ptr(running_mean),
-                                 _ptr(running_var), float(momentum), float(eps), _ptr(ws), _ptr(stats),
-                                 ctypes.c_void_p(y.data_ptr()), _stream(x.device)))
+        y, stats = bn_forward(x, weight, bias, running_mean, running_var, momentum, eps, relu)
         ctx.save_for_backward(x, weight, stats)
+        ctx.relu = bool(relu)
         return y
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, gy):
-        lib = load_library()
         x, weight, stats = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
-        M = x.numel() // 64
-        ws = torch.empty(lib.bk_bn_workspace_doubles(), dtype=torch.float64, device=x.device)
-        coef = torch.empty(256, dtype=torch.float32, device=x.device)
-        dg = torch.empty(64, dtype=torch.float32, device=x.device)
-        db = torch.empty(64, dtype=torch.float32, device=x.device)
-        dx = torch.empty_like(x, memory_format=torch.channels_last)
-        _check(lib.bk_bn_backward(ctypes.c_void_p(gy.data_ptr()), ctypes.c_void_p(x.data_ptr()), M, _ptr(weight),
-                                  _ptr(stats), _ptr(ws), _ptr(coef), _ptr(dg), _ptr(db), ctypes.c_void_p(dx.data_ptr()),
-                                  _stream(x.device)))
-        return dx, dg, db, None, None, None, None
+        dx, dg, db, _ = bn_backward(gy, x, weight, stats, ctx.relu, False)
+        return dx, dg, db, None, None, None, None, None
+
+
+class ConvBNFunction(torch.autograd.Function):
+    """y = [relu](bn(conv(x))) in training (models/blokus_nnet.py:103-112's conv -> BatchNorm2d (->
+    ReLU)): the conv on bk_conv_x3 (+ bias), the batch norm and ReLU on bk_bn_forward_ex; the
+    backward on bk_bn_backward_ex — the ReLU's mask, dgamma, dbeta and the conv's bias gradient
+    (dx's column sums, in the same pass) — then the conv's input gradient (bk_conv_x3, flipped
+    weights) and weight gradient (bk_conv_x3_wgrad). Saves what the unfused pair saves (x, the conv
+    output) and moves two fewer activation passes each way (the separate ReLU and bias sums)."""
+
+    @staticmethod
+    def forward(ctx, x, cw, cb, gamma, beta, running_mean, running_var, momentum, eps, relu):
+        ws, inv = pack_weight(cw, flip=False)
+        x = x.contiguous(memory_format=torch.channels_last)
+        z = conv_x3(x, ws, inv, cb)
+        y, stats = bn_forward(z, gamma, beta, running_mean, running_var, momentum, eps, relu)
+        ctx.save_for_backward(x, cw, z, gamma, stats)
+        ctx.relu, ctx.has_bias = bool(relu), cb is not None
+        return y
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gy):
+        x, cw, z, gamma, stats = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        need_cb = ctx.has_bias and ctx.needs_input_grad[2]
+        dz, dg, db, dcb = bn_backward(gy, z, gamma, stats, ctx.relu, need_cb)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            ws, inv = pack_weight(cw, flip=True)
+            gx = conv_x3(dz, ws, inv, None)
+        if ctx.needs_input_grad[1]:
+            gw = conv_x3_wgrad(x, dz)
+        return gx, gw, dcb, dg, db, None, None, None, None, None
 
 
 class FusedBatchNorm2d(NativeBatchNorm2d):
@@ -144,7 +197,7 @@ class FusedBatchNorm2d(NativeBatchNorm2d):
                 and x.numel() > 64):
             self.num_batches_tracked.add_(1)
             return BatchNormFunction.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                           self.momentum, self.eps)
+                                           self.momentum, self.eps, False)
         return super().forward(x)
 
 
@@ -187,6 +240,60 @@ def use_x3_convs(model: nn.Module) -> int:
     return k
 
 
+def _bn_ok(bn: nn.Module) -> bool:
+    return (isinstance(bn, nn.BatchNorm2d) and bn.num_features == 64 and bn.affine and bn.track_running_stats
+            and bn.momentum is not None)
+
+
+def _bn_apply(bn: nn.Module, x: torch.Tensor, relu: bool) -> torch.Tensor:
+    bn.num_batches_tracked.add_(1)
+    return BatchNormFunction.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, relu)
+
+
+def _conv_bn(conv: nn.Module, bn: nn.Module, x: torch.Tensor, relu: bool) -> torch.Tensor:
+    bn.num_batches_tracked.add_(1)
+    return ConvBNFunction.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                bn.momentum, bn.eps, relu)
+
+
+class TrainResNet(ResNet):
+    """nets.ResNet (same modules, parameters and state_dict keys) whose training forward (train
+    mode, gradients enabled, 20x20 f32 on the device) runs each residual block's conv -> BN -> ReLU
+    and conv -> BN as one ConvBNFunction each and the stem's BN -> ReLU as one BatchNormFunction,
+    and returns the policy head's raw logits instead of their log-softmax: the learner's loss is
+    the masked log-softmax over the legal ids (bk_policy_loss, neural_network.py:138-157), which is
+    invariant to the dense log-softmax's per-row shift, and its gradient sums to zero over a row,
+    so the dense log-softmax (a [B, A] pass each way) changes neither the loss nor the gradients.
+    Every other forward (eval, no_grad, CPU) is ResNet's own."""
+
+    def _fused_ok(self, x: torch.Tensor) -> bool:
+        return (self.training and torch.is_grad_enabled() and x.is_cuda and x.dtype == torch.float32
+                and x.dim() == 4 and x.shape[2] == 20 and x.shape[3] == 20 and _bn_ok(self.bn1)
+                and all(_eligible_x3(b[0]) and _eligible_x3(b[3]) and _bn_ok(b[1]) and _bn_ok(b[4])
+                        and isinstance(b[2], nn.ReLU) and len(b) == 5 for b in self.res_blocks))
+
+    def forward(self, x):
+        if not self._fused_ok(x):
+            return super().forward(x)
+        x = _bn_apply(self.bn1, self.conv1(x).contiguous(memory_format=torch.channels_last), True)
+        h = x
+        for b in self.res_blocks:
+            h = _conv_bn(b[0], b[1], h, True)
+            h = _conv_bn(b[3], b[4], h, False)
+        x = F.relu(x + h)
+        p = F.relu(self.policy_bn(self.policy_conv(x))).flatten(1)
+        p = self.policy_out(p)  # raw logits (see the class docstring)
+        v = F.relu(self.value_bn(self.value_conv(x))).flatten(1)
+        v = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
+        return p, v
+
+
+def _eligible_x3(m: nn.Module) -> bool:
+    return isinstance(m, nn.Conv2d) and m.in_channels == 64 and m.out_channels == 64 and m.kernel_size == (3, 3) \
+        and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1) and m.groups == 1 \
+        and m.padding_mode == "zeros"
+
+
 def prepare_model(model: nn.Module, x3_convs: bool = True, fused_bn: bool = True) -> nn.Module:
     """The device training path IN PLACE on the caller's model (Learner(device_path="auto") calls
     it): channels_last parameters, PyTorch batch norm (the 64-channel ones on bk_bn_forward /
@@ -198,4 +305,6 @@ def prepare_model(model: nn.Module, x3_convs: bool = True, fused_bn: bool = True
         use_fused_batchnorm(model)
     if x3_convs:
         use_x3_convs(model)
+    if x3_convs and fused_bn and type(model) is ResNet:
+        model.__class__ = TrainResNet  # the block-level fusion (conv + BN + ReLU per autograd node)
     return model.to(memory_format=torch.channels_last)

@@ -14,24 +14,39 @@ namespace {
 using f32x4 = float __attribute__((ext_vector_type(4)));
 constexpr int kBnThreads = 256, kBnRows = kBnThreads / 16;  // 16 channel quads x 16 rows per pass
 constexpr int kBnGrid = 512;
+constexpr int kBnAxGrid = 2048;  // k_bn_axpb's workgroups (grid-stride)
 
 // per workgroup: sum over its rows of a[r][c] (and of a[r][c] * (b[r][c] - mb[c]) when b != null,
 // else of a[r][c]^2) in fp64 -> part[g][c][2]
+// (rp, rq non-null, the fused ReLU's backward: a counts only where b rp + rq > 0, i.e. where the
+// forward's batch-norm output was positive)
 __global__ __launch_bounds__(kBnThreads) void k_bn_reduce(const float* __restrict__ a, const float* __restrict__ b,
                                                           const float* __restrict__ mb, int64_t M,
-                                                          double* __restrict__ part) {
+                                                          double* __restrict__ part, const float* __restrict__ rp,
+                                                          const float* __restrict__ rq) {
   __shared__ double red[kBnRows][64][2];
   const int tid = threadIdx.x, q = tid & 15, rl = tid >> 4;
   const f32x4* a4 = reinterpret_cast<const f32x4*>(a);
   const f32x4* b4 = reinterpret_cast<const f32x4*>(b);
-  f32x4 m4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 m4 = {0.f, 0.f, 0.f, 0.f}, p4 = {0.f, 0.f, 0.f, 0.f}, q4 = {0.f, 0.f, 0.f, 0.f};
   if (b) m4 = reinterpret_cast<const f32x4*>(mb)[q];
+  if (rp) {
+    p4 = reinterpret_cast<const f32x4*>(rp)[q];
+    q4 = reinterpret_cast<const f32x4*>(rq)[q];
+  }
   double s[4] = {0, 0, 0, 0}, t[4] = {0, 0, 0, 0};
   for (int64_t r = (int64_t)blockIdx.x * kBnRows + rl; r < M; r += (int64_t)gridDim.x * kBnRows) {
     const f32x4 v = __builtin_nontemporal_load(a4 + r * 16 + q);
-    const float vv[4] = {v.x, v.y, v.z, v.w};
+    float vv[4] = {v.x, v.y, v.z, v.w};
     if (b) {
       const f32x4 w = __builtin_nontemporal_load(b4 + r * 16 + q);
+      if (rp) {
+        const f32x4 z = w * p4 + q4;
+        vv[0] = z.x > 0.f ? vv[0] : 0.f;
+        vv[1] = z.y > 0.f ? vv[1] : 0.f;
+        vv[2] = z.z > 0.f ? vv[2] : 0.f;
+        vv[3] = z.w > 0.f ? vv[3] : 0.f;
+      }
       const float ww[4] = {w.x - m4.x, w.y - m4.y, w.z - m4.z, w.w - m4.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -136,21 +151,75 @@ __global__ __launch_bounds__(kBnFinThreads) void k_bn_finalize_bwd(const double*
 }
 
 // out = a * p[c] + q[c] (+ b * r[c]) over [M][64] (forward: y = x scale + shift; backward:
-// dx = dy k1 + k2 + x k3)
+// dx = dy k1 + k2 + x k3). relu: out = max(out, 0) (the fused ReLU of the forward). mp / mq
+// non-null (the fused ReLU's backward): a counts only where b mp + mq > 0. colsum non-null: the
+// workgroup's per-channel sums of out in fp64 -> colsum[g][c][0] (the bias gradient of the conv
+// that feeds the batch norm, k_colsum_finalize adds them up in a fixed order).
 __global__ __launch_bounds__(256) void k_bn_axpb(const float* __restrict__ a, const float* __restrict__ b,
                                                  const float* __restrict__ p, const float* __restrict__ q,
-                                                 const float* __restrict__ rr, int64_t n4, float* __restrict__ out) {
+                                                 const float* __restrict__ rr, int64_t n4, float* __restrict__ out,
+                                                 int relu, const float* __restrict__ mp, const float* __restrict__ mq,
+                                                 double* __restrict__ colsum) {
   const f32x4* a4 = reinterpret_cast<const f32x4*>(a);
   const f32x4* b4 = reinterpret_cast<const f32x4*>(b);
   const int cq = threadIdx.x & 15;  // the channel quad is fixed per thread: the stride is a multiple of 16
   const f32x4 pv = reinterpret_cast<const f32x4*>(p)[cq], qv = reinterpret_cast<const f32x4*>(q)[cq];
-  f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+  f32x4 rv = {0.f, 0.f, 0.f, 0.f}, mpv = {0.f, 0.f, 0.f, 0.f}, mqv = {0.f, 0.f, 0.f, 0.f};
   if (b) rv = reinterpret_cast<const f32x4*>(rr)[cq];
+  if (mp) {
+    mpv = reinterpret_cast<const f32x4*>(mp)[cq];
+    mqv = reinterpret_cast<const f32x4*>(mq)[cq];
+  }
+  double cs[4] = {0, 0, 0, 0};
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    f32x4 v = __builtin_nontemporal_load(a4 + i) * pv + qv;
-    if (b) v += __builtin_nontemporal_load(b4 + i) * rv;
+    f32x4 av = __builtin_nontemporal_load(a4 + i);
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (b) bv = __builtin_nontemporal_load(b4 + i);
+    if (mp) {
+      const f32x4 z = bv * mpv + mqv;
+      av.x = z.x > 0.f ? av.x : 0.f;
+      av.y = z.y > 0.f ? av.y : 0.f;
+      av.z = z.z > 0.f ? av.z : 0.f;
+      av.w = z.w > 0.f ? av.w : 0.f;
+    }
+    f32x4 v = av * pv + qv;
+    if (b) v += bv * rv;
+    if (relu) {
+      v.x = v.x > 0.f ? v.x : 0.f;
+      v.y = v.y > 0.f ? v.y : 0.f;
+      v.z = v.z > 0.f ? v.z : 0.f;
+      v.w = v.w > 0.f ? v.w : 0.f;
+    }
+    if (colsum) {
+      cs[0] += (double)v.x;
+      cs[1] += (double)v.y;
+      cs[2] += (double)v.z;
+      cs[3] += (double)v.w;
+    }
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out) + i);
   }
+  if (colsum) {  // workgroup-uniform
+    __shared__ double red[16][64];
+    const int rl = threadIdx.x >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[rl][4 * cq + j] = cs[j];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      double acc = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc += red[i][threadIdx.x];
+      colsum[((size_t)blockIdx.x * 64 + threadIdx.x) * 2] = acc;
+      colsum[((size_t)blockIdx.x * 64 + threadIdx.x) * 2 + 1] = 0.0;
+    }
+  }
+}
+
+// colsum partials [G][64][2] -> out[c] (f32), in bn_sum_parts' fixed order
+__global__ __launch_bounds__(kBnFinThreads) void k_colsum_finalize(const double* __restrict__ part, int G,
+                                                                   float* __restrict__ outc) {
+  double s0, s1;
+  bn_sum_parts(part, G, s0, s1);
+  if (threadIdx.x < 64) outc[threadIdx.x] = (float)s0;
 }
 
 }  // namespace
@@ -162,9 +231,11 @@ extern "C" {
 
 int bk_bn_workspace_doubles(void) { return kBnGrid * 64 * 2; }
 
-int bk_bn_forward(const float* x, int64_t M, const float* gamma, const float* beta, float* running_mean,
-                  float* running_var, float momentum, float eps, double* workspace, float* stats, float* y,
-                  void* stream) {
+int bk_bn_workspace2_doubles(void) { return kBnAxGrid * 64 * 2; }
+
+int bk_bn_forward_ex(const float* x, int64_t M, const float* gamma, const float* beta, float* running_mean,
+                     float* running_var, float momentum, float eps, double* workspace, float* stats, float* y, int relu,
+                     void* stream) {
   BK_REQUIRE(x && workspace && stats && y && M > 0, "bad argument");
   BK_REQUIRE(((uintptr_t)x & 15u) == 0 && ((uintptr_t)y & 15u) == 0 && ((uintptr_t)stats & 15u) == 0,
              "bk_bn_forward: 16-byte aligned buffers");
@@ -172,32 +243,50 @@ int bk_bn_forward(const float* x, int64_t M, const float* gamma, const float* be
   const int64_t blocks = (M + kBnRows - 1) / kBnRows;
   const int G = blocks < kBnGrid ? (int)blocks : kBnGrid;
   hipLaunchKernelGGL(k_bn_reduce, dim3(G), dim3(kBnThreads), 0, s, x, (const float*)nullptr, (const float*)nullptr, M,
-                     workspace);
+                     workspace, (const float*)nullptr, (const float*)nullptr);
   hipLaunchKernelGGL(k_bn_finalize_fwd, dim3(1), dim3(kBnFinThreads), 0, s, workspace, G, M, gamma, beta, running_mean, running_var,
                      momentum, eps, stats);
   const int64_t n4 = M * 16;
   const int64_t ab = (n4 + 255) / 256;
-  hipLaunchKernelGGL(k_bn_axpb, dim3(ab < 2048 ? (int)ab : 2048), dim3(256), 0, s, x, (const float*)nullptr, stats + 128,
-                     stats + 192, (const float*)nullptr, n4, y);
+  hipLaunchKernelGGL(k_bn_axpb, dim3(ab < kBnAxGrid ? (int)ab : kBnAxGrid), dim3(256), 0, s, x, (const float*)nullptr,
+                     stats + 128, stats + 192, (const float*)nullptr, n4, y, relu, (const float*)nullptr,
+                     (const float*)nullptr, (double*)nullptr);
   return launch_check("bk_bn_forward");
 }
 
-int bk_bn_backward(const float* dy, const float* x, int64_t M, const float* gamma, const float* stats, double* workspace,
-                   float* coef, float* dgamma, float* dbeta, float* dx, void* stream) {
+int bk_bn_forward(const float* x, int64_t M, const float* gamma, const float* beta, float* running_mean,
+                  float* running_var, float momentum, float eps, double* workspace, float* stats, float* y,
+                  void* stream) {
+  return bk_bn_forward_ex(x, M, gamma, beta, running_mean, running_var, momentum, eps, workspace, stats, y, 0, stream);
+}
+
+int bk_bn_backward_ex(const float* dy, const float* x, int64_t M, const float* gamma, const float* stats,
+                      double* workspace, float* coef, float* dgamma, float* dbeta, float* dx, int relu, float* dsum,
+                      double* workspace2, void* stream) {
   BK_REQUIRE(dy && x && stats && workspace && coef && dx && M > 0, "bad argument");
+  BK_REQUIRE(!dsum || workspace2, "bk_bn_backward_ex: dsum needs workspace2");
   BK_REQUIRE(((uintptr_t)dy & 15u) == 0 && ((uintptr_t)x & 15u) == 0 && ((uintptr_t)dx & 15u) == 0 &&
                  ((uintptr_t)coef & 15u) == 0 && ((uintptr_t)stats & 15u) == 0,
              "bk_bn_backward: 16-byte aligned buffers");
   hipStream_t s = (hipStream_t)stream;
   const int64_t blocks = (M + kBnRows - 1) / kBnRows;
   const int G = blocks < kBnGrid ? (int)blocks : kBnGrid;
-  hipLaunchKernelGGL(k_bn_reduce, dim3(G), dim3(kBnThreads), 0, s, dy, x, stats, M, workspace);
+  const float* mp = relu ? stats + 128 : nullptr;
+  const float* mq = relu ? stats + 192 : nullptr;
+  hipLaunchKernelGGL(k_bn_reduce, dim3(G), dim3(kBnThreads), 0, s, dy, x, stats, M, workspace, mp, mq);
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3(1), dim3(kBnFinThreads), 0, s, workspace, G, M, gamma, stats, dgamma, dbeta, coef);
   const int64_t n4 = M * 16;
   const int64_t ab = (n4 + 255) / 256;
-  hipLaunchKernelGGL(k_bn_axpb, dim3(ab < 2048 ? (int)ab : 2048), dim3(256), 0, s, dy, x, coef, coef + 64, coef + 128, n4,
-                     dx);
+  const int GA = ab < kBnAxGrid ? (int)ab : kBnAxGrid;
+  hipLaunchKernelGGL(k_bn_axpb, dim3(GA), dim3(256), 0, s, dy, x, coef, coef + 64, coef + 128, n4, dx, 0, mp, mq,
+                     dsum ? workspace2 : (double*)nullptr);
+  if (dsum) hipLaunchKernelGGL(k_colsum_finalize, dim3(1), dim3(kBnFinThreads), 0, s, workspace2, GA, dsum);
   return launch_check("bk_bn_backward");
+}
+
+int bk_bn_backward(const float* dy, const float* x, int64_t M, const float* gamma, const float* stats, double* workspace,
+                   float* coef, float* dgamma, float* dbeta, float* dx, void* stream) {
+  return bk_bn_backward_ex(dy, x, M, gamma, stats, workspace, coef, dgamma, dbeta, dx, 0, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

@@ -313,6 +313,19 @@ int bk_bn_forward(const float* x, int64_t M, const float* gamma, const float* be
                   void* stream);
 int bk_bn_backward(const float* dy, const float* x, int64_t M, const float* gamma, const float* stats, double* workspace,
                    float* coef, float* dgamma, float* dbeta, float* dx, void* stream);
+/* The same with the block's ReLU fused (models/blokus_nnet.py:103-112 / :137: relu(bn(conv(x))))
+ * and the feeding conv's bias gradient: bk_bn_forward_ex with relu != 0 writes y = max(bn(x), 0);
+ * bk_bn_backward_ex with relu != 0 takes dy = the ReLU output's gradient (masked where the
+ * forward's bn(x) was not positive, recomputed from x and stats: no extra read); dsum (may be
+ * NULL) receives the per-channel sum of dx over the M rows (= the bias gradient of the conv whose
+ * output x is), summed in fp64 in a fixed order; workspace2: bk_bn_workspace2_doubles() doubles. */
+int bk_bn_workspace2_doubles(void);
+int bk_bn_forward_ex(const float* x, int64_t M, const float* gamma, const float* beta, float* running_mean,
+                     float* running_var, float momentum, float eps, double* workspace, float* stats, float* y, int relu,
+                     void* stream);
+int bk_bn_backward_ex(const float* dy, const float* x, int64_t M, const float* gamma, const float* stats,
+                      double* workspace, float* coef, float* dgamma, float* dbeta, float* dx, int relu, float* dsum,
+                      double* workspace2, void* stream);
 
 /* ---------------------------------------------------------------- PPO
  * PPOTrainer._compute_gae (ppo/trainer.py:177-211) + returns = advantages + values (:83) for a

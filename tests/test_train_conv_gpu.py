@@ -260,3 +260,72 @@ def test_learner_device_path_tracks_fp32():
     # "auto" picks the device path at large batches on the GPU only
     assert Learner(ResNet(20, 4, eng.A, 1).cuda(), batch_size=64).device_path is False
     assert Learner(ResNet(20, 4, eng.A, 1).cuda(), batch_size=1024).device_path is True
+
+
+def test_fused_conv_bn_relu_matches_fp64():
+    """ConvBNFunction (conv on bk_conv_x3 -> batch norm + ReLU on bk_bn_forward_ex; backward with the
+    ReLU mask recomputed from the conv output and the conv's bias gradient as dx's column sums)
+    against the fp64 conv -> BatchNorm2d -> ReLU: output, dx, dW, dgamma, dbeta at fp32-class
+    tolerances; the conv bias gradient (zero in exact arithmetic under train-mode batch norm) to
+    1e-6 of the summed |dz| scale; relu off as well."""
+    from blokus_rl_amd.alphazero.train_conv import ConvBNFunction
+
+    g = torch.Generator().manual_seed(9)
+    for relu in (True, False):
+        x = torch.randn(33, 64, 20, 20, generator=g, dtype=torch.float64)
+        w = torch.randn(64, 64, 3, 3, generator=g, dtype=torch.float64) * 0.05
+        b = torch.randn(64, generator=g, dtype=torch.float64) * 0.1
+        gam = torch.rand(64, generator=g, dtype=torch.float64) + 0.5
+        bet = torch.randn(64, generator=g, dtype=torch.float64) * 0.2
+        gy = torch.randn(33, 64, 20, 20, generator=g, dtype=torch.float64)
+        xr, wr, br, gr, btr = (t.clone().requires_grad_() for t in (x, w, b, gam, bet))
+        z = F.conv2d(xr, wr, br, padding=1)
+        yr = F.batch_norm(z, torch.zeros(64, dtype=torch.float64), torch.ones(64, dtype=torch.float64), gr, btr,
+                          training=True, momentum=0.1, eps=1e-5)
+        if relu:
+            yr = F.relu(yr)
+        yr.backward(gy)
+        xd = x.float().cuda().contiguous(memory_format=torch.channels_last).requires_grad_()
+        wd, bd, gd, btd = (t.float().cuda().requires_grad_() for t in (w, b, gam, bet))
+        rm, rv = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+        y = ConvBNFunction.apply(xd, wd, bd, gd, btd, rm, rv, 0.1, 1e-5, relu)
+        y.backward(gy.float().cuda().contiguous(memory_format=torch.channels_last))
+        scale = lambda t: float(t.abs().max())  # noqa: E731
+        assert float((y.detach().double().cpu() - yr.detach()).abs().max()) <= 5e-6 * scale(yr.detach())
+        for a, r in ((xd.grad, xr.grad), (wd.grad, wr.grad), (gd.grad, gr.grad), (btd.grad, btr.grad)):
+            assert float((a.double().cpu() - r).abs().max()) <= 2e-5 * scale(r), (relu, scale(r))
+        assert float(bd.grad.abs().max()) <= 1e-6 * float(gy.abs().sum(dim=(0, 2, 3)).max())
+        assert float((rm.double().cpu() - 0.1 * z.detach().mean(dim=(0, 2, 3))).abs().max()) <= 1e-6 * float(z.abs().max())
+
+
+def test_train_resnet_matches_unfused_device_path():
+    """TrainResNet (block-level fusion + raw policy logits) against the same model with the fusion
+    off (the per-module device path), one step through the reference loss: the losses agree to
+    1e-6 relative, the parameter gradients to 1e-4 of each gradient's norm (the conv biases that
+    feed a batch norm aside: rounding noise on both paths)."""
+    from blokus_rl_amd.alphazero.learner import alphazero_loss
+    from blokus_rl_amd.alphazero.train_conv import TrainResNet, prepare_model
+    from blokus_rl_amd.nets import ResNet
+
+    eng, rb = _replay()
+    idx = torch.randint(0, 512, (256,), device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    batch = rb.batch(idx)
+    out = {}
+    for fused in (True, False):
+        torch.manual_seed(0)
+        model = prepare_model(ResNet(20, 4, eng.A, 2).cuda())
+        assert isinstance(model, TrainResNet)
+        if not fused:
+            model.__class__ = ResNet
+        model.train()
+        p, v = model(batch["observation"].contiguous(memory_format=torch.channels_last))
+        loss = alphazero_loss(p, v, batch)
+        loss.backward()
+        out[fused] = (float(loss), {k: t.grad.detach().clone() for k, t in model.named_parameters()})
+    assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0])
+    for k, g0 in out[False][1].items():
+        if k in ("conv1.bias", "policy_conv.bias", "value_conv.bias") or (
+                k.startswith("res_blocks") and k.endswith(".bias") and k.split(".")[2] in ("0", "3")):
+            continue  # the bias of a conv that feeds a batch norm: zero in exact arithmetic
+        d = (out[True][1][k] - g0).norm()
+        assert float(d) <= 1e-4 * float(g0.norm()) + 1e-12, (k, float(d), float(g0.norm()))

@@ -8,5 +8,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from blokus_rl_amd.alphazero.learner_bench import bench_learner  # noqa: E402
 from blokus_rl_amd.engine import Engine  # noqa: E402
 
-r = bench_learner(Engine(20, 4, 5), 1, 0, 1024, 10, 3, rows=8192, device_path="auto")
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+r = bench_learner(Engine(20, 4, 5), 1, 0, 1024, steps, 3, rows=8192, device_path="auto")
 print("device_path", r["device_path"], "elapsed", r["elapsed_s"])
