@@ -62,6 +62,20 @@ def policy_loss(x: torch.Tensor, ids: torch.Tensor, pi: torch.Tensor, k: torch.T
     return PolicyLoss.apply(x, ids, pi, k)
 
 
+_IDENT: dict = {}
+
+
+def sparse_policy_loss(xs: torch.Tensor, pi: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
+    """policy_loss on logits already gathered at the rows' legal ids (xs [B, cap]: column j = the
+    logit of ids[b][j], SparsePolicyLinear): the same kernels with the identity id map."""
+    B, cap = xs.shape
+    key = (xs.device, B, cap)
+    ident = _IDENT.get(key)
+    if ident is None:
+        ident = _IDENT[key] = torch.arange(cap, dtype=torch.int16, device=xs.device).expand(B, cap).contiguous()
+    return PolicyLoss.apply(xs, ident, pi, k)
+
+
 def alphazero_loss(p_pred, v_pred, batch, policy_fn=policy_loss):
     """compute_loss (neural_network.py:138-157): policy cross-entropy over the legal ids + value
     MSE `(v_pred.squeeze() - z).pow(2).mean()`."""
@@ -130,8 +144,12 @@ class Learner:
             device_path = on_gpu and batch_size >= 256
         self.device_path = bool(device_path)
         if self.device_path:
-            from .train_conv import prepare_model
+            from .train_conv import TrainResNet, prepare_model
             prepare_model(model)
+            # the policy Linear at the batch's legal ids only (trainfc.hip), with the reference loss
+            self.sparse_head = isinstance(model, TrainResNet) and policy_fn is policy_loss
+        else:
+            self.sparse_head = False
         self.policy_fn = policy_fn
         self.group = group
         up = dist.is_available() and dist.is_initialized()
@@ -152,8 +170,12 @@ class Learner:
         obs = batch["observation"]
         if self.device_path:
             obs = obs.contiguous(memory_format=torch.channels_last)
-        p_pred, v_pred = self.net(obs)
-        loss = alphazero_loss(p_pred, v_pred, batch, self.policy_fn)
+        if self.sparse_head:
+            xs, v_pred = self.net(obs, ids=batch["ids"], k=batch["k"])
+            loss = sparse_policy_loss(xs, batch["pi"], batch["k"]) + (v_pred.squeeze() - batch["score"]).pow(2).mean()
+        else:
+            p_pred, v_pred = self.net(obs)
+            loss = alphazero_loss(p_pred, v_pred, batch, self.policy_fn)
         self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
         self.optimizer.step()

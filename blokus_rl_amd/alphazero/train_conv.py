@@ -240,6 +240,53 @@ def use_x3_convs(model: nn.Module) -> int:
     return k
 
 
+class SparsePolicyLinear(torch.autograd.Function):
+    """The policy Linear at each row's legal ids only (trainfc.hip): xs[b][j] = bias[ids[b][j]] +
+    pf[b] . W[ids[b][j]] for j < k[b] — the logits compute_loss reads (neural_network.py:138-157);
+    the backward's input gradient and dense weight / bias gradients (zero at ids no row holds) from
+    the same pairs, in a fixed order."""
+
+    @staticmethod
+    def forward(ctx, pf, W, bias, ids, k):
+        lib = load_library()
+        pf = pf.float().contiguous()
+        B, F = pf.shape
+        cap = ids.shape[1]
+        xs = torch.empty((B, cap), dtype=torch.float32, device=pf.device)
+        _check(lib.bk_sparse_linear_fwd(_ptr(pf), B, F, _ptr(W.detach()), _ptr(bias.detach()), _ptr(ids), _ptr(k), cap,
+                                        _ptr(xs), _stream(pf.device)))
+        ctx.save_for_backward(pf, W, ids, k)
+        return xs
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g):
+        lib = load_library()
+        pf, W, ids, k = ctx.saved_tensors
+        g = g.float().contiguous()
+        B, F = pf.shape
+        A, cap = W.shape[0], ids.shape[1]
+        dev, st = pf.device, _stream(pf.device)
+        dpf = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dpf = torch.empty_like(pf)
+            _check(lib.bk_sparse_linear_dx(_ptr(g), B, F, _ptr(W.detach()), _ptr(ids), _ptr(k), cap, _ptr(dpf), st))
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            count = torch.zeros(A, dtype=torch.int32, device=dev)
+            _check(lib.bk_sparse_linear_index(_ptr(ids), _ptr(k), cap, B, A, _ptr(count), None, None, None, st))
+            start = torch.zeros(A + 1, dtype=torch.int32, device=dev)
+            start[1:] = torch.cumsum(count, 0, dtype=torch.int32)
+            cursor = torch.zeros(A, dtype=torch.int32, device=dev)
+            pairs = torch.empty(B * cap, dtype=torch.int32, device=dev)
+            _check(lib.bk_sparse_linear_index(_ptr(ids), _ptr(k), cap, B, A, _ptr(count), _ptr(start), _ptr(cursor),
+                                              _ptr(pairs), st))
+            dW = torch.empty((A, F), dtype=torch.float32, device=dev)
+            db = torch.empty(A, dtype=torch.float32, device=dev)
+            _check(lib.bk_sparse_linear_dw(_ptr(g), _ptr(pf), B, F, cap, A, _ptr(start), _ptr(pairs), _ptr(dW), _ptr(db),
+                                           st))
+        return dpf, dW, db, None, None
+
+
 def _bn_ok(bn: nn.Module) -> bool:
     return (isinstance(bn, nn.BatchNorm2d) and bn.num_features == 64 and bn.affine and bn.track_running_stats
             and bn.momentum is not None)
@@ -272,8 +319,13 @@ class TrainResNet(ResNet):
                 and all(_eligible_x3(b[0]) and _eligible_x3(b[3]) and _bn_ok(b[1]) and _bn_ok(b[4])
                         and isinstance(b[2], nn.ReLU) and len(b) == 5 for b in self.res_blocks))
 
-    def forward(self, x):
+    def forward(self, x, ids: torch.Tensor | None = None, k: torch.Tensor | None = None):
+        """ids / k (the batch's legal ids [B, cap] int16 and counts [B] int32): the policy head
+        returns the logits at those ids only, [B, cap] (SparsePolicyLinear; the learner's loss reads
+        nothing else), instead of the dense raw logits."""
         if not self._fused_ok(x):
+            if ids is not None:
+                raise ValueError("the sparse policy head is the device training path's (train mode, grad, cuda)")
             return super().forward(x)
         x = _bn_apply(self.bn1, self.conv1(x).contiguous(memory_format=torch.channels_last), True)
         h = x
@@ -282,7 +334,10 @@ class TrainResNet(ResNet):
             h = _conv_bn(b[3], b[4], h, False)
         x = F.relu(x + h)
         p = F.relu(self.policy_bn(self.policy_conv(x))).flatten(1)
-        p = self.policy_out(p)  # raw logits (see the class docstring)
+        if ids is not None:
+            p = SparsePolicyLinear.apply(p, self.policy_out.weight, self.policy_out.bias, ids, k)
+        else:
+            p = self.policy_out(p)  # raw logits (see the class docstring)
         v = F.relu(self.value_bn(self.value_conv(x))).flatten(1)
         v = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
         return p, v

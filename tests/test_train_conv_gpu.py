@@ -329,3 +329,81 @@ def test_train_resnet_matches_unfused_device_path():
             continue  # the bias of a conv that feeds a batch norm: zero in exact arithmetic
         d = (out[True][1][k] - g0).norm()
         assert float(d) <= 1e-4 * float(g0.norm()) + 1e-12, (k, float(d), float(g0.norm()))
+
+
+def test_sparse_policy_linear_matches_dense():
+    """SparsePolicyLinear (trainfc.hip) against the dense Linear followed by the gather at the rows'
+    legal ids, in fp64: the gathered logits, and the input / weight / bias gradients from an upstream
+    gradient that lives on the legal ids only (what the masked loss produces). Rows of 0 and of
+    `cap` ids, ids shared by many rows (the counting-sort index) and ids no row holds (zero rows of
+    dW); deterministic (two runs bitwise equal)."""
+    from blokus_rl_amd.alphazero.train_conv import SparsePolicyLinear
+
+    g = torch.Generator().manual_seed(21)
+    B, F, A, cap = 300, 800, 3000, 128
+    pf = torch.relu(torch.randn(B, F, generator=g, dtype=torch.float64))
+    W = torch.randn(A, F, generator=g, dtype=torch.float64) * 0.03
+    bias = torch.randn(A, generator=g, dtype=torch.float64) * 0.1
+    k = torch.randint(0, cap + 1, (B,), generator=g)
+    k[0], k[1] = 0, cap
+    ids = torch.full((B, cap), -1, dtype=torch.int16)
+    for b in range(B):
+        pool = 600 if b % 2 else A  # half the rows draw from a small pool: shared ids
+        ids[b, : int(k[b])] = torch.randperm(pool, generator=g)[: int(k[b])].sort().values.to(torch.int16)
+    valid = torch.arange(cap)[None, :] < k[:, None]
+    gy = torch.randn(B, cap, generator=g, dtype=torch.float64) * valid
+    # fp64 dense reference
+    pr, Wr, br = (t.clone().requires_grad_() for t in (pf, W, bias))
+    dense = torch.nn.functional.linear(pr, Wr, br)
+    gat = torch.gather(dense, 1, ids.long().clamp(min=0)) * valid
+    gat.backward(gy)
+    outs = []
+    for _ in range(2):
+        pd, Wd, bd = (t.float().cuda().requires_grad_() for t in (pf, W, bias))
+        xs = SparsePolicyLinear.apply(pd, Wd, bd, ids.cuda(), k.to(torch.int32).cuda())
+        xs.backward(gy.float().cuda())
+        outs.append((xs.detach().cpu(), pd.grad.cpu(), Wd.grad.cpu(), bd.grad.cpu()))
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))  # deterministic
+    xs, dpf, dW, db = (t.double() for t in outs[0])
+    assert float(((xs - gat.detach()) * valid).abs().max()) <= 1e-5 * float(gat.detach().abs().max())
+    assert float((xs * ~valid).abs().max()) == 0.0
+    for a, r in ((dpf, pr.grad), (dW, Wr.grad), (db, br.grad)):
+        assert float((a - r).abs().max()) <= 1e-5 * float(r.abs().max()), float((a - r).abs().max())
+    held = torch.zeros(A, dtype=torch.bool)
+    held[ids[valid].long()] = True
+    assert bool((dW[~held] == 0).all()) and bool((db[~held] == 0).all()) and int((~held).sum()) > 0
+
+
+def test_learner_sparse_head_matches_dense_head():
+    """The learner's step with the sparse policy head (Learner.sparse_head: logits at the legal ids
+    only) against the same device path with the dense raw logits: loss to 1e-6 relative, every
+    parameter gradient to 1e-4 of its norm (conv biases that feed a batch norm aside)."""
+    from blokus_rl_amd.alphazero.learner import Learner, alphazero_loss, sparse_policy_loss
+    from blokus_rl_amd.nets import ResNet
+
+    eng, rb = _replay()
+    idx = torch.randint(0, 512, (256,), device="cuda", generator=torch.Generator(device="cuda").manual_seed(8))
+    batch = rb.batch(idx)
+    out = {}
+    for sparse in (True, False):
+        torch.manual_seed(0)
+        model = ResNet(20, 4, eng.A, 2).cuda()
+        L = Learner(model, batch_size=256, device_path=True)
+        assert L.sparse_head
+        model.train()
+        obs = batch["observation"].contiguous(memory_format=torch.channels_last)
+        if sparse:
+            xs, v = model(obs, ids=batch["ids"], k=batch["k"])
+            loss = sparse_policy_loss(xs, batch["pi"], batch["k"]) + (v.squeeze() - batch["score"]).pow(2).mean()
+        else:
+            p, v = model(obs)
+            loss = alphazero_loss(p, v, batch)
+        loss.backward()
+        out[sparse] = (float(loss), {n: t.grad.detach().clone() for n, t in model.named_parameters()})
+    assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0])
+    for n, g0 in out[False][1].items():
+        if n in ("conv1.bias", "policy_conv.bias", "value_conv.bias") or (
+                n.startswith("res_blocks") and n.endswith(".bias") and n.split(".")[2] in ("0", "3")):
+            continue
+        d = (out[True][1][n] - g0).norm()
+        assert float(d) <= 1e-4 * float(g0.norm()) + 1e-12, (n, float(d), float(g0.norm()))
