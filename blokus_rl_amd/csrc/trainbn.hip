@@ -76,36 +76,30 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_reduce(const float* __restric
   }
 }
 
-// the per-workgroup partial sums part[g][c][2] added over g: 1024 threads = 64 channels x 16 slices
-// of g (8 loads in flight per thread), the 16 slices then combined in order; thread c < 64 gets its
-// channel's two totals
-constexpr int kBnFinThreads = 1024, kBnSlices = kBnFinThreads / 64;
+// the per-workgroup partial sums part[g][c][2] added over g for channel c = blockIdx.x (one
+// workgroup per channel: 256 threads each take g = tid, tid + 256, ... in order, then a fixed
+// LDS tree); every thread gets the channel's two totals
+constexpr int kBnFinThreads = 256;
 __device__ __forceinline__ void bn_sum_parts(const double* __restrict__ part, int G, double& s0, double& s1) {
-  __shared__ double red[kBnSlices][64][2];
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int g = sl * 8;
-  for (; g + 8 <= G; g += 8 * kBnSlices) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      a[j] += part[((size_t)(g + j) * 64 + c) * 2];
-      b[j] += part[((size_t)(g + j) * 64 + c) * 2 + 1];
-    }
+  __shared__ double red[kBnFinThreads][2];
+  const int c = blockIdx.x, t = threadIdx.x;
+  double a = 0, b = 0;
+  for (int g = t; g < G; g += kBnFinThreads) {
+    a += part[((size_t)g * 64 + c) * 2];
+    b += part[((size_t)g * 64 + c) * 2 + 1];
   }
-  for (int j = 0; g + j < G && j < 8; ++j) {
-    a[j] += part[((size_t)(g + j) * 64 + c) * 2];
-    b[j] += part[((size_t)(g + j) * 64 + c) * 2 + 1];
-  }
-  red[sl][c][0] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  red[sl][c][1] = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
+  red[t][0] = a;
+  red[t][1] = b;
   __syncthreads();
-  s0 = 0;
-  s1 = 0;
-#pragma unroll
-  for (int i = 0; i < kBnSlices; ++i) {
-    s0 += red[i][c][0];
-    s1 += red[i][c][1];
+  for (int h = kBnFinThreads / 2; h > 0; h >>= 1) {
+    if (t < h) {
+      red[t][0] += red[t + h][0];
+      red[t][1] += red[t + h][1];
+    }
+    __syncthreads();
   }
+  s0 = red[0][0];
+  s1 = red[0][1];
 }
 
 // forward statistics -> mean, invstd, scale = gamma invstd, shift = beta - mean scale (f32), and
@@ -114,10 +108,10 @@ __global__ __launch_bounds__(kBnFinThreads) void k_bn_finalize_fwd(const double*
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
                                                          float eps, float* __restrict__ stats) {
-  const int c = threadIdx.x;
+  const int c = blockIdx.x;
   double s, ss;
   bn_sum_parts(part, G, s, ss);
-  if (c >= 64) return;
+  if (threadIdx.x != 0) return;
   const double mean = s / (double)M;
   double var = ss / (double)M - mean * mean;
   var = var > 0 ? var : 0;
@@ -136,10 +130,10 @@ __global__ __launch_bounds__(kBnFinThreads) void k_bn_finalize_bwd(const double*
                                                          const float* __restrict__ gamma, const float* __restrict__ stats,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                          float* __restrict__ coef) {
-  const int c = threadIdx.x;
+  const int c = blockIdx.x;
   double sd, sdx;  // sum dy, sum dy (x - mean)
   bn_sum_parts(part, G, sd, sdx);
-  if (c >= 64) return;
+  if (threadIdx.x != 0) return;
   const double mean = stats[c], inv = stats[64 + c], g = gamma ? gamma[c] : 1.0f;
   if (dgamma) dgamma[c] = (float)(sdx * inv);
   if (dbeta) dbeta[c] = (float)sd;
@@ -214,12 +208,12 @@ __global__ __launch_bounds__(256) void k_bn_axpb(const float* __restrict__ a, co
   }
 }
 
-// colsum partials [G][64][2] -> out[c] (f32), in bn_sum_parts' fixed order
+// colsum partials [G][64][2] -> out[c] (f32), in bn_sum_parts' fixed order (64 workgroups)
 __global__ __launch_bounds__(kBnFinThreads) void k_colsum_finalize(const double* __restrict__ part, int G,
                                                                    float* __restrict__ outc) {
   double s0, s1;
   bn_sum_parts(part, G, s0, s1);
-  if (threadIdx.x < 64) outc[threadIdx.x] = (float)s0;
+  if (threadIdx.x == 0) outc[blockIdx.x] = (float)s0;
 }
 
 }  // namespace
@@ -244,7 +238,7 @@ int bk_bn_forward_ex(const float* x, int64_t M, const float* gamma, const float*
   const int G = blocks < kBnGrid ? (int)blocks : kBnGrid;
   hipLaunchKernelGGL(k_bn_reduce, dim3(G), dim3(kBnThreads), 0, s, x, (const float*)nullptr, (const float*)nullptr, M,
                      workspace, (const float*)nullptr, (const float*)nullptr);
-  hipLaunchKernelGGL(k_bn_finalize_fwd, dim3(1), dim3(kBnFinThreads), 0, s, workspace, G, M, gamma, beta, running_mean, running_var,
+  hipLaunchKernelGGL(k_bn_finalize_fwd, dim3(64), dim3(kBnFinThreads), 0, s, workspace, G, M, gamma, beta, running_mean, running_var,
                      momentum, eps, stats);
   const int64_t n4 = M * 16;
   const int64_t ab = (n4 + 255) / 256;
@@ -274,13 +268,13 @@ int bk_bn_backward_ex(const float* dy, const float* x, int64_t M, const float* g
   const float* mp = relu ? stats + 128 : nullptr;
   const float* mq = relu ? stats + 192 : nullptr;
   hipLaunchKernelGGL(k_bn_reduce, dim3(G), dim3(kBnThreads), 0, s, dy, x, stats, M, workspace, mp, mq);
-  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3(1), dim3(kBnFinThreads), 0, s, workspace, G, M, gamma, stats, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3(64), dim3(kBnFinThreads), 0, s, workspace, G, M, gamma, stats, dgamma, dbeta, coef);
   const int64_t n4 = M * 16;
   const int64_t ab = (n4 + 255) / 256;
   const int GA = ab < kBnAxGrid ? (int)ab : kBnAxGrid;
   hipLaunchKernelGGL(k_bn_axpb, dim3(GA), dim3(256), 0, s, dy, x, coef, coef + 64, coef + 128, n4, dx, 0, mp, mq,
                      dsum ? workspace2 : (double*)nullptr);
-  if (dsum) hipLaunchKernelGGL(k_colsum_finalize, dim3(1), dim3(kBnFinThreads), 0, s, workspace2, GA, dsum);
+  if (dsum) hipLaunchKernelGGL(k_colsum_finalize, dim3(64), dim3(kBnFinThreads), 0, s, workspace2, GA, dsum);
   return launch_check("bk_bn_backward");
 }
 
