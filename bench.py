@@ -531,9 +531,10 @@ def bench_vecenv(args, world, rank):
     torch.cuda.synchronize()
     eager = E * 200 / (time.perf_counter() - te)
     # PPO-style: the agent's actions drawn from policy logits each step (the rollout's
-    # get_action_and_value + env.step, ppo/trainer.py:144-155) — bk_vec_policy (FilterLegalMoves +
-    # Categorical sample + log_prob in one launch) then k_vec_step7, replayed from a HIP graph of
-    # `per` such pairs; the logits row is the actor's output stand-in (random, [E, A] f32 in HBM)
+    # get_action_and_value + env.step, ppo/trainer.py:144-155) — the draw (FilterLegalMoves +
+    # Categorical sample + log_prob) fused into k_vec_step7 (bk_vec_step_policy), replayed from a
+    # HIP graph of `per` steps; the logits row is the actor's output stand-in (random, [E, A] f32 in
+    # HBM). Beside it the draw alone (k_vec_policy, the standalone kernel).
     logits = (torch.randn((E, env.eng.A), device=env.device, generator=torch.Generator(env.device).manual_seed(rank))
               * 2.0).contiguous()
     gp, gs = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -546,6 +547,7 @@ def bench_vecenv(args, world, rank):
     gp.replay()
     gs.replay()
     torch.cuda.synchronize()
+    kbar = float(env.valid_mask().sum()) / E  # the agent's mean legal-id count on these boards
     reps2 = max(1, args.vec_steps // per)
     _barrier(world)
     t1 = time.perf_counter()
@@ -580,7 +582,11 @@ def bench_vecenv(args, world, rank):
         torch_step()
     torch.cuda.synchronize()
     torch_ops = E * 50 / (time.perf_counter() - tt)
-    pol_bytes = 4 * env.eng.A + 8 * env.eng.W + 16 + 8
+    # algorithmic bytes: the fused step = the env step's 393 B + the legal ids' logits (4 B each, the
+    # only ones read) + the id and log-prob out; the standalone draw = its logits row reads of the
+    # legal ids + the 120-B mask + rng 16 + out 8
+    fused_bytes = VEC_BYTES_PER_STEP + 4.0 * kbar + 8
+    pol_bytes = 4.0 * kbar + 8 * env.eng.W + 16 + 8
     achieved = VEC_BYTES_PER_STEP * E / (kernel_ms * 1e-3)
     # the headline is the DEVICE rate (graph-replayed launches, in-kernel agent draws); a gym-style
     # loop calling env.step() per step gets eager_env_step_calls (one launch + tensor bookkeeping
@@ -594,13 +600,19 @@ def bench_vecenv(args, world, rank):
                               "comparable with rounds <= 3",
            "with_masked_policy_sampling": {
                "value": E * n2 * world / dt2, "unit": "env-steps/s", "steps": n2,
-               "path": "bk_vec_policy (FilterLegalMoves + Categorical sample + log_prob, one launch) -> k_vec_step7, "
-                       "HIP-graph-replayed pairs; logits [E, A] f32 resident in HBM (the actor's output stand-in)",
-               "ms_per_step": pair_ms,
-               "roofline": {"bound": "hbm", "kernel": "k_vec_policy", "achieved": pol_bytes * E / (pol_ms * 1e-3) / 1e9,
-                            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": pol_bytes * E / (pol_ms * 1e-3) / HBM_PEAK,
-                            "kernel_ms": pol_ms, "bytes_per_unit": pol_bytes, "units_per_launch": E,
-                            "traffic": _pmc_traffic("k_vec_policy", E)},
+               "path": "k_vec_step7<policy> (bk_vec_step_policy: FilterLegalMoves + Categorical sample + log_prob "
+                       "fused into the env step), HIP-graph-replayed; logits [E, A] f32 resident in HBM (the actor's "
+                       "output stand-in)",
+               "ms_per_step": pair_ms, "legal_ids_per_env": kbar,
+               "roofline": {"bound": "hbm", "kernel": "k_vec_step7<policy>",
+                            "achieved": fused_bytes * E / (pair_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                            "unit": "GB/s", "frac": fused_bytes * E / (pair_ms * 1e-3) / HBM_PEAK,
+                            "kernel_ms": pair_ms, "bytes_per_unit": fused_bytes, "units_per_launch": E,
+                            "traffic": _pmc_traffic("k_vec_step7_policy", E)},
+               "draw_alone": {"kernel": "k_vec_policy", "kernel_ms": pol_ms, "bytes_per_unit": pol_bytes,
+                              "achieved": pol_bytes * E / (pol_ms * 1e-3) / 1e9, "unit": "GB/s",
+                              "frac": pol_bytes * E / (pol_ms * 1e-3) / HBM_PEAK,
+                              "traffic": _pmc_traffic("k_vec_policy", E)},
                "torch_ops_eager": {"value": torch_ops, "unit": "env-steps/s",
                                    "note": "round-5 path: valid_mask + torch.where(-1e9) + Categorical.sample/log_prob + "
                                            "env.step per step"}},

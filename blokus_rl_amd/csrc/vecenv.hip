@@ -287,6 +287,184 @@ __device__ __forceinline__ int kth_bit64(uint64_t x64, int k) {
   return pos;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The agent's move drawn from its policy, as the reference's PPO rollout draws it
+// (ppo/trainer.py:144-155 -> CnnAgent.get_action_and_value, ppo/agent.py:148-156: the actor's
+// logits through FilterLegalMoves, :27-42, then Categorical(logits).sample() and .log_prob()), by
+// the 16 lanes of an env: fused into the env step (k_vec_step7<.., POL>, which has the agent's
+// legal mask in registers at the step's start) and standalone (k_vec_policy, mask words from HBM).
+// Lane j owns mask words w = j, j + 16, ... (< W64); its candidates are those words' set bits
+// (ids ascending), minus ids whose logit is exactly 0 under the reference filter's quirk; with no
+// candidate in the env, every id in [0, A) at logit -1e9 (the reference's all -1e9 row: uniform).
+// Only the candidates' logits are read (~22 of 919 per env on config-5 boards). The draw is an
+// inverse CDF with a fixed, restatable arithmetic (oracle/vecenv_oracle.py policy_sample):
+//   m = max candidate logit (16-lane butterfly); p = bk_expf(x - m); s_j = lane j's sum, ids
+//   ascending; incl = 16-lane Hillis-Steele scan (DPP row_shr 1, 2, 4, 8); S = incl_15;
+//   u = (z >> 40) 2^-24 from the env's splitmix64 stream (one draw, before the opponent's);
+//   target = S u; lane = first with incl > target (else the last with s > 0); inside it, walking
+//   from incl_{lane-1}: the first candidate whose running sum passes the target (else its last
+//   p > 0); logp = x_a - (m + bk_logf(S))  (torch's logsumexp form: the all -1e9 row gives 0).
+// exp / log from + - * / only (-ffp-contract=off): bitwise reproducible by numpy float32.
+__device__ __forceinline__ float bk_expf(float x) {  // x <= 0; below -80 (e^-80 < 2^-115): 0
+  if (!(x >= -80.0f)) return 0.0f;
+  const float n = __builtin_rintf(x * 1.44269502f);
+  const float r = (x - n * 0.693145752f) - n * 1.42860677e-6f;
+  float p = 1.38888892e-3f;
+  p = p * r + 8.33333377e-3f;
+  p = p * r + 4.16666679e-2f;
+  p = p * r + 0.166666672f;
+  p = p * r + 0.5f;
+  p = p * r + 1.0f;
+  p = p * r + 1.0f;
+  return p * __int_as_float(((int)n + 127) << 23);
+}
+__device__ __forceinline__ float bk_logf(float x) {  // x >= 1, finite
+  const int bits = __float_as_int(x);
+  int e = ((bits >> 23) & 255) - 127;
+  float f = __int_as_float((bits & 0x7FFFFF) | 0x3F800000);  // [1, 2)
+  if (f > 1.41421354f) {
+    f = f * 0.5f;
+    e += 1;
+  }
+  const float s = (f - 1.0f) / (f + 1.0f);
+  const float s2 = s * s;
+  float q = 0.111111112f;
+  q = q * s2 + 0.142857149f;
+  q = q * s2 + 0.200000003f;
+  q = q * s2 + 0.333333343f;
+  q = q * s2 + 1.0f;
+  return (float)e * 0.693147182f + (2.0f * s) * q;
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// -> the drawn id (the same in the env's 16 lanes; A when every logit was non-finite: the env then
+// takes it as an illegal move), logp in every lane; st advanced by one draw. wd: lane j's words.
+template <int W64, int A, bool ZQ>
+__device__ __forceinline__ int policy_draw16(const float* __restrict__ row, const uint64_t (&wd)[(W64 + 15) / 16],
+                                             uint64_t& st, float& logp) {
+  constexpr int NW = (W64 + 15) / 16;
+  constexpr int CAPW = NW == 1 ? 8 : 4;  // candidates per word whose logits load up front
+  const int l = lane_id(), j = l & 15, gb = l & ~15;
+  float xr[NW][CAPW];
+  int idr[NW][CAPW], nr[NW];
+  uint64_t rem[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    uint64_t b = (j + 16 * i < W64) ? wd[i] : 0ull;
+    nr[i] = 0;
+#pragma unroll
+    for (int c = 0; c < CAPW; ++c) {
+      const int pos = b ? __ffsll((unsigned long long)b) - 1 : 0;
+      idr[i][c] = 64 * (j + 16 * i) + pos;
+      nr[i] += b ? 1 : 0;
+      b &= b - 1ull;
+    }
+    rem[i] = b;
+#pragma unroll
+    for (int c = 0; c < CAPW; ++c) xr[i][c] = c < nr[i] ? row[idr[i][c]] : 0.0f;
+  }
+  // every candidate in order: f(x, id) (the register ones, then the rest of the word: rare)
+  auto each = [&](auto&& f) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+#pragma unroll
+      for (int c = 0; c < CAPW; ++c)
+        if (c < nr[i] && (!ZQ || xr[i][c] != 0.0f)) f(xr[i][c], idr[i][c]);
+      uint64_t b = rem[i];
+      while (b) {
+        const int id = 64 * (j + 16 * i) + __ffsll((unsigned long long)b) - 1;
+        b &= b - 1ull;
+        const float x = row[id];
+        if (!ZQ || x != 0.0f) f(x, id);
+      }
+    }
+  };
+  float m = -INFINITY;
+  bool has = false;
+  each([&](float x, int) {
+    m = fmaxf(m, x);
+    has = true;
+  });
+  const bool none = ((__ballot(has) >> gb) & 0xFFFFull) == 0ull;  // group-uniform
+  m = fmaxf(m, dppf<0xB1>(m));
+  m = fmaxf(m, dppf<0x4E>(m));
+  m = fmaxf(m, dppf<0x141>(m));
+  m = fmaxf(m, dppf<0x140>(m));
+  if (none) m = -1e9f;
+  // valid ids of the lane's words (the no-candidate row)
+  int nvalid = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int w = j + 16 * i, lim = A - 64 * w;
+    nvalid += w < W64 ? (lim >= 64 ? 64 : lim) : 0;
+  }
+  float s = 0.0f;
+  if (none) {
+    for (int c = 0; c < nvalid; ++c) s = s + 1.0f;
+  } else {
+    each([&](float x, int) { s = s + bk_expf(x - m); });
+  }
+  float incl = s, t = dppf<0x111>(incl);
+  if (j >= 1) incl = t + incl;
+  t = dppf<0x112>(incl);
+  if (j >= 2) incl = t + incl;
+  t = dppf<0x114>(incl);
+  if (j >= 4) incl = t + incl;
+  t = dppf<0x118>(incl);
+  if (j >= 8) incl = t + incl;
+  const float S = __shfl(incl, gb + 15);
+  const uint64_t z = mix64(st);  // = the env's splitmix64 output (rng_index's draw)
+  st += 0x9E3779B97F4A7C15ull;
+  const float target = S * ((float)(uint32_t)(z >> 40) * 0x1p-24f);
+  const uint32_t over = (uint32_t)((__ballot(incl > target) >> gb) & 0xFFFFull);
+  const uint32_t pos = (uint32_t)((__ballot(s > 0.0f) >> gb) & 0xFFFFull);
+  const int sel = over ? __ffs(over) - 1 : (pos ? 31 - __clz(pos) : 0);
+  const float excl = __shfl(incl, gb + (sel > 0 ? sel - 1 : 0));
+  int pick = -1;
+  float xp = 0.0f;
+  if (j == sel) {
+    float acc = sel > 0 ? excl : 0.0f;
+    if (none) {
+      for (int c = 0; c < nvalid; ++c) {
+        acc = acc + 1.0f;
+        if (acc > target) {
+          pick = 64 * (j + 16 * (c >> 6)) + (c & 63);
+          break;
+        }
+      }
+      if (pick < 0 && nvalid > 0) pick = 64 * (j + 16 * ((nvalid - 1) >> 6)) + ((nvalid - 1) & 63);
+      xp = -1e9f;
+    } else {
+      int last = -1;
+      float xl = 0.0f;
+      each([&](float x, int id) {
+        if (pick >= 0) return;
+        const float p = bk_expf(x - m);
+        if (p > 0.0f) {
+          acc = acc + p;
+          last = id;
+          xl = x;
+          if (acc > target) {
+            pick = id;
+            xp = x;
+          }
+        }
+      });
+      if (pick < 0) {
+        pick = last;
+        xp = xl;
+      }
+    }
+  }
+  pick = __shfl(pick, gb + sel);
+  xp = __shfl(xp, gb + sel);
+  logp = pick >= 0 ? xp - (m + bk_logf(S)) : __int_as_float(0x7FC00000);
+  return pick >= 0 ? pick : A;
+}
+
 #ifdef BK_VEC_STAMP
 // diagnostic build only: per wave (lane 0), s_memtime at the phases of k_vec_step7 (bk_vec_stamps)
 __device__ unsigned long long g_vec_stamps[4096][8];
@@ -303,11 +481,18 @@ __device__ unsigned long long g_vec_stamps[4096][8];
   } while (0)
 #endif
 
-template <int MC, int G>
+// POL (G = 16 only): 0 = the agent's id given (actions) or drawn uniformly; 1 / 2 = drawn from
+// its policy logits by policy_draw16 (2: with the reference filter's zero-logit quirk), the id and
+// its log-prob written to act_out / logp_out
+template <int MC, int G, int POL = 0>
 __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uint64_t* rng,
                                                           const int32_t* __restrict__ actions, int E,
                                                           uint8_t* __restrict__ obs, uint64_t* __restrict__ mask,
-                                                          float* __restrict__ reward, int32_t* __restrict__ done) {
+                                                          float* __restrict__ reward, int32_t* __restrict__ done,
+                                                          const float* __restrict__ logits = nullptr,
+                                                          int32_t* __restrict__ act_out = nullptr,
+                                                          float* __restrict__ logp_out = nullptr) {
+  static_assert(POL == 0 || G == 16, "the policy draw runs on 16 lanes per env");
   using V = Vec7<MC, G>;
   constexpr int NL = V::NL, kVecEnvsPerBlock = V::EPB;
   __shared__ uint32_t m32[kVecEnvsPerBlock][V::W32 + 1];
@@ -469,11 +654,51 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
     to_move = next;
   };
 
+  // each orientation's legal origins compacted from stride-8 rows to its (R x W)-bit field
+  // (<= 49 bits), ORed into the env's LDS words at the orientation's first id (<= 3 words)
+  auto assemble = [&]() {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u);
+      uint64_t f = 0;
+#pragma unroll
+      for (int r = 0; r < 7; ++r) f |= (uint64_t)((uint32_t)(L[i] >> (8 * r)) & 0x7Fu) << (r * W);
+      if (f) {
+        const int w = base >> 5, sh = base & 31;
+        const uint64_t x = f << sh;
+        const uint32_t x2 = sh ? (uint32_t)(f >> (64 - sh)) : 0u;
+        if ((uint32_t)x) atomicOr(&m32[le][w], (uint32_t)x);
+        if ((uint32_t)(x >> 32)) atomicOr(&m32[le][w + 1], (uint32_t)(x >> 32));
+        if (x2) atomicOr(&m32[le][w + 2], x2);
+      }
+    }
+  };
+
   float rew = 0.0f;
   int fin = 0;
-  const int a = actions ? actions[es] : -1;
+  int a = actions ? actions[es] : -1;
   const int K0 = legal(0);  // the agent (colour 0) is to move at every step start
   VSTAMP(1);
+  if (POL) {  // the agent's id drawn from its policy over its legal mask (assembled in LDS)
+    wave_lds_sync();  // the group's zeroing of its words (kernel start) is done
+    assemble();
+    wave_lds_sync();
+    constexpr int NW = (V::W64 + 15) / 16;
+    uint64_t wd[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int w = j + 16 * i;
+      wd[i] = w < V::W64 ? ((uint64_t)m32[le][2 * w] | ((uint64_t)m32[le][2 * w + 1] << 32)) : 0ull;
+    }
+    float lp;
+    a = policy_draw16<V::W64, V::A, POL == 2>(logits + (size_t)es * V::A, wd, st, lp);
+    if (live && j == 4) {
+      act_out[e] = a;
+      logp_out[e] = lp;
+    }
+    wave_lds_sync();  // every lane has read the words
+    for (int w = j; w < V::W32 + 1; w += G) m32[le][w] = 0u;  // re-zeroed for the output mask
+  }
   // the agent's move: the given id if it is legal, else (a < 0) a uniformly random legal one
   Pick pk = a >= 0 ? decode(a) : (K0 > 0 ? kth((int)rng_index(&st, K0)) : Pick{-1, 0u, 0u, 0});
   if (pk.id < 0) {  // an illegal agent action (or no legal move) ends the episode as a loss
@@ -550,24 +775,9 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
 #pragma unroll
       for (int c = 0; c < 7; ++c) ob[le * 49 + j * 7 + c] = ((r0 >> c) & 1u) ? 1 : (((r1 >> c) & 1u) ? 2 : 0);
     }
-    // mask: each orientation's legal origins compacted from stride-8 rows to its (R x W)-bit field
-    // (<= 49 bits), ORed into the env's LDS words at the orientation's first id (<= 3 words)
-    wave_lds_sync();  // the group's zeroing of its words (kernel start) is done
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int base = (int)(meta[i] & 0xFFFu), W = (int)((meta[i] >> 17) & 7u);
-      uint64_t f = 0;
-#pragma unroll
-      for (int r = 0; r < 7; ++r) f |= (uint64_t)((uint32_t)(L[i] >> (8 * r)) & 0x7Fu) << (r * W);
-      if (f) {
-        const int w = base >> 5, sh = base & 31;
-        const uint64_t x = f << sh;
-        const uint32_t x2 = sh ? (uint32_t)(f >> (64 - sh)) : 0u;
-        if ((uint32_t)x) atomicOr(&m32[le][w], (uint32_t)x);
-        if ((uint32_t)(x >> 32)) atomicOr(&m32[le][w + 1], (uint32_t)(x >> 32));
-        if (x2) atomicOr(&m32[le][w + 2], x2);
-      }
-    }
+    // mask: the agent's legal origins as the env's LDS words
+    wave_lds_sync();  // the group's zeroing of its words is done
+    assemble();
   }
   VSTAMP(5);
   __syncthreads();
@@ -590,129 +800,29 @@ __global__ __launch_bounds__(kVecThreads) void k_vec_step7(uint32_t* states, uin
   VSTAMP(7);
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_vec_policy: the agent's move drawn from its policy, as the reference's PPO rollout draws it
-// (ppo/trainer.py:144-155 -> CnnAgent.get_action_and_value, ppo/agent.py:148-156: the actor's
-// logits through FilterLegalMoves, :27-42, then Categorical(logits).sample() and .log_prob()).
-// One wave per env: lane l loads ids 64 t + l (t < T), one coalesced 256-B row segment per load;
-// mask word t is wave-uniform (a scalar load), so a lane's candidate test is one bit of it. The
-// candidates are the legal ids (minus those whose logit is exactly 0 under the reference filter's
-// quirk); with none, every id in [0, A) at logit -1e9 (the reference's all -1e9 row: uniform).
-// The K candidates are compacted in ascending id order into the wave's LDS slots (mask word +
-// mbcnt rank; ~22 of 919 ids on the config-5 boards, mostly one slot per lane),
-// so the exponentials run on K / 64 slots per lane instead of all T x 64 ids (VALU-bound
-// otherwise: ~8 % of a 7x7 row is legal). The draw is an inverse CDF with a fixed, restatable
-// arithmetic (oracle/vecenv_oracle.py policy_sample):
-//   m = max candidate logit; p_j = bk_expf(x_j - m) for slot j; s_l = sum over slots l, l + 64,
-//   ... in order; incl = BK_WAVE_SCAN of s (DPP order); S = incl_63; u = (z >> 40) 2^-24 from the
-//   env's splitmix64 stream (one draw; the env's own stream, as the opponent's moves);
-//   target = S u; lane = first with incl > target (else the last with s > 0); walking its slots
-//   from incl_{lane-1}: the first whose running sum passes the target (else its last p > 0);
-//   logp = x_a - (m + bk_logf(S))  (torch's logsumexp form, so the all -1e9 row gives 0 as there).
-// Bound: HBM (the [E][A] f32 logits row, 4 B per id).
-// exp / log from + - * / only (-ffp-contract=off): bitwise reproducible by numpy float32.
-__device__ __forceinline__ float bk_expf(float x) {  // x <= 0; below -80 (e^-80 < 2^-115): 0
-  if (!(x >= -80.0f)) return 0.0f;
-  const float n = __builtin_rintf(x * 1.44269502f);
-  const float r = (x - n * 0.693145752f) - n * 1.42860677e-6f;
-  float p = 1.38888892e-3f;
-  p = p * r + 8.33333377e-3f;
-  p = p * r + 4.16666679e-2f;
-  p = p * r + 0.166666672f;
-  p = p * r + 0.5f;
-  p = p * r + 1.0f;
-  p = p * r + 1.0f;
-  return p * __int_as_float(((int)n + 127) << 23);
-}
-__device__ __forceinline__ float bk_logf(float x) {  // x >= 1, finite
-  const int bits = __float_as_int(x);
-  int e = ((bits >> 23) & 255) - 127;
-  float f = __int_as_float((bits & 0x7FFFFF) | 0x3F800000);  // [1, 2)
-  if (f > 1.41421354f) {
-    f = f * 0.5f;
-    e += 1;
-  }
-  const float s = (f - 1.0f) / (f + 1.0f);
-  const float s2 = s * s;
-  float q = 0.111111112f;
-  q = q * s2 + 0.142857149f;
-  q = q * s2 + 0.200000003f;
-  q = q * s2 + 0.333333343f;
-  q = q * s2 + 1.0f;
-  return (float)e * 0.693147182f + (2.0f * s) * q;
-}
-
-template <int T, int AC, bool ZQ>  // AC: the id count at compile time (the 7x7 presets), 0 = runtime A
-__global__ __launch_bounds__(256) void k_vec_policy(const float* __restrict__ logits, int A_, int W64_,
-                                                    const uint64_t* __restrict__ mask, uint64_t* __restrict__ rng,
-                                                    int E, int32_t* __restrict__ act, float* __restrict__ logp) {
-  const int A = AC ? AC : A_, W64 = AC ? (AC + 63) / 64 : W64_;
-  extern __shared__ __attribute__((aligned(16))) float pol_lds[];
-  float* xs = pol_lds + (threadIdx.x >> 6) * (T * 64);                                                // slot logits
-  uint16_t* is = reinterpret_cast<uint16_t*>(pol_lds + 4 * T * 64) + (threadIdx.x >> 6) * (T * 64);  // slot ids
-  const int e = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-  if (e >= E) return;  // wave-uniform
-  const int l = lane_id();
-  const float* row = logits + (size_t)e * A;
-  const uint64_t* mw = mask + (size_t)e * W64;
-  uint64_t st = rng[e];
-  float x[T];
+// k_vec_policy: policy_draw16 alone (the rollout's draw without the step: the agent's legal mask
+// words from HBM, as bk_vec_reset / bk_vec_step leave them); 16 lanes per env, 16 envs per block.
+template <int MC, bool ZQ>
+__global__ __launch_bounds__(kVecThreads) void k_vec_policy(const float* __restrict__ logits,
+                                                            const uint64_t* __restrict__ mask,
+                                                            uint64_t* __restrict__ rng, int E,
+                                                            int32_t* __restrict__ act, float* __restrict__ logp) {
+  using V = Vec7<MC, 16>;
+  constexpr int NW = (V::W64 + 15) / 16;
+  const int j = threadIdx.x & 15, e = blockIdx.x * (kVecThreads / 16) + (threadIdx.x >> 4);
+  const int es = e < E ? e : E - 1;  // a spare lane group mirrors the last env and stores nothing
+  uint64_t wd[NW];
 #pragma unroll
-  for (int t = 0; t < T; ++t) x[t] = (t < W64 && 64 * t + l < A) ? row[64 * t + l] : 0.0f;
-  // compaction, word by word: the candidates of word t are the mask word itself (wave-uniform,
-  // in SGPRs) limited to ids < A (and, under the quirk, to lanes whose logit is not 0); a zero
-  // word costs a scalar test only. Slot K + rank (mbcnt) gets (logit, id).
-  int K = 0;
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int lim = A - 64 * t;
-    uint64_t b = t < W64 ? mw[t] : 0ull;
-    b &= lim >= 64 ? ~0ull : (lim > 0 ? (1ull << lim) - 1ull : 0ull);
-    if (b != 0ull) {  // wave-uniform
-      if (ZQ) b &= __ballot(x[t] != 0.0f);
-      if ((b >> l) & 1ull) {
-        const int j = K + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        xs[j] = x[t];
-        is[j] = (uint16_t)(64 * t + l);
-      }
-      K += __popcll(b);
-    }
+  for (int i = 0; i < NW; ++i) {
+    const int w = j + 16 * i;
+    wd[i] = w < V::W64 ? mask[(size_t)es * V::W64 + w] : 0ull;
   }
-  const bool none = K == 0;  // no candidate: the all -1e9 row, slot j = id j (no LDS)
-  if (none) K = A;
-  wave_lds_sync();
-  float m = -INFINITY;
-  for (int j = l; j < K; j += kWave) m = fmaxf(m, none ? -1e9f : xs[j]);
-  m = wave_max_f(m);
-  float s = 0.0f;
-  for (int j = l; j < K; j += kWave) s = s + bk_expf((none ? -1e9f : xs[j]) - m);
-  float incl = s;
-  BK_WAVE_SCAN(incl, dpp_f, op_add_f);
-  const float S = readlane_f(incl, kWave - 1);
-  const uint64_t z = mix64(st);  // = the env's splitmix64 output (rng_index's draw)
-  st += 0x9E3779B97F4A7C15ull;
-  const float target = S * ((float)(uint32_t)(z >> 40) * 0x1p-24f);
-  const uint64_t over = __ballot(incl > target), pos = __ballot(s > 0.0f);
-  const int sel = over ? __ffsll((unsigned long long)over) - 1 : (pos ? 63 - __clzll((long long)pos) : 0);
-  const float excl = sel > 0 ? readlane_f(incl, sel - 1) : 0.0f;
-  if (l == sel) {
-    float acc = excl;
-    int pick = -1, last = -1;
-    for (int j = l; j < K; j += kWave) {
-      const float p = bk_expf((none ? -1e9f : xs[j]) - m);
-      if (p > 0.0f) {
-        acc = acc + p;
-        last = j;
-        if (acc > target) {
-          pick = j;
-          break;
-        }
-      }
-    }
-    if (pick < 0) pick = last;
-    // pick < 0 only for non-finite logits: an out-of-range id (the env's illegal-move loss)
-    act[e] = pick < 0 ? A : (none ? pick : (int)is[pick]);
-    logp[e] = pick < 0 ? __int_as_float(0x7FC00000) : (none ? -1e9f : xs[pick]) - (m + bk_logf(S));
+  uint64_t st = rng[es];
+  float lp;
+  const int a = policy_draw16<V::W64, V::A, ZQ>(logits + (size_t)es * V::A, wd, st, lp);
+  if (e < E && j == 0) {
+    act[e] = a;
+    logp[e] = lp;
     rng[e] = st;
   }
 }
@@ -776,28 +886,46 @@ int bk_vec_step(bk_ctx* c, void* states, uint64_t* rng, const int32_t* actions, 
 int bk_vec_policy(bk_ctx* c, const float* logits, const uint64_t* mask, uint64_t* rng, int E, int zero_masked,
                   int32_t* actions, float* logp, void* stream) {
   BK_REQUIRE(c && logits && mask && rng && actions && logp && E >= 0, "bad argument");
-  BK_REQUIRE(c->dp.W64 <= 64, "policy sampling holds <= 64 x 64 ids per env (the 2-player 7x7 presets)");
+  BK_REQUIRE(c->dp.P == 2 && c->dp.N == 7 && (c->dp.num_pieces == 9 || c->dp.num_pieces == 21),
+             "policy sampling: the 2-player 7x7 presets (919 / 2522 ids)");
   if (E == 0) return BK_OK;
-  const dim3 grid((E + 3) / 4), block(256);
+  const dim3 grid((E + 15) / 16), block(kVecThreads);
   hipStream_t st = (hipStream_t)stream;
-  const int A = c->dp.A, W = c->dp.W64;
-  // per wave: T x 64 slots of (f32 logit, u16 id)
-#define BK_POL(T, AC)                                                                                        \
-  if (zero_masked)                                                                                           \
-    hipLaunchKernelGGL((k_vec_policy<T, AC, true>), grid, block, 4 * (T) * 64 * 6, st, logits, A, W, mask, rng, \
-                       E, actions, logp);                                                                     \
-  else                                                                                                       \
-    hipLaunchKernelGGL((k_vec_policy<T, AC, false>), grid, block, 4 * (T) * 64 * 6, st, logits, A, W, mask, rng, \
-                       E, actions, logp)
-  if (A == 919) {
-    BK_POL(15, 919);
-  } else if (A == 2522) {
-    BK_POL(40, 2522);
+  if (c->dp.num_pieces == 9) {
+    if (zero_masked)
+      hipLaunchKernelGGL((k_vec_policy<4, true>), grid, block, 0, st, logits, mask, rng, E, actions, logp);
+    else
+      hipLaunchKernelGGL((k_vec_policy<4, false>), grid, block, 0, st, logits, mask, rng, E, actions, logp);
   } else {
-    BK_POL(64, 0);
+    if (zero_masked)
+      hipLaunchKernelGGL((k_vec_policy<5, true>), grid, block, 0, st, logits, mask, rng, E, actions, logp);
+    else
+      hipLaunchKernelGGL((k_vec_policy<5, false>), grid, block, 0, st, logits, mask, rng, E, actions, logp);
   }
-#undef BK_POL
   return launch_check("k_vec_policy");
+}
+
+int bk_vec_step_policy(bk_ctx* c, void* states, uint64_t* rng, const float* logits, int zero_masked, int E,
+                       uint8_t* obs, uint64_t* mask, float* reward, int32_t* done, int32_t* actions, float* logp,
+                       void* stream) {
+  BK_REQUIRE(c && states && rng && logits && obs && mask && reward && done && actions && logp && E >= 0,
+             "bad argument");
+  BK_REQUIRE(c->dp.P == 2 && c->dp.N == 7 && (c->dp.num_pieces == 9 || c->dp.num_pieces == 21),
+             "the fused policy step: the 2-player 7x7 presets (919 / 2522 ids)");
+  if (E == 0) return BK_OK;
+  const dim3 grid((E + kVecThreads / 16 - 1) / (kVecThreads / 16));
+  hipStream_t st = (hipStream_t)stream;
+  uint32_t* sp = (uint32_t*)states;
+#define BK_SP(MC, P)                                                                                              \
+  hipLaunchKernelGGL((k_vec_step7<MC, 16, P>), grid, dim3(kVecThreads), 0, st, sp, rng, (const int32_t*)nullptr, E, \
+                     obs, mask, reward, done, logits, actions, logp)
+  if (c->dp.num_pieces == 9) {
+    if (zero_masked) BK_SP(4, 2); else BK_SP(4, 1);
+  } else {
+    if (zero_masked) BK_SP(5, 2); else BK_SP(5, 1);
+  }
+#undef BK_SP
+  return launch_check("k_vec_step7<policy>");
 }
 
 }  // extern "C"

@@ -61,6 +61,7 @@ _SIGS = {
     "bk_vec_reset": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "bk_vec_step": (_i, [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "bk_vec_policy": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "bk_vec_step_policy": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bk_replay_stride": (ctypes.c_size_t, [_i]),
     "bk_replay_batch": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bk_policy_loss": (_i, [_vp, ctypes.c_int64, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp]),

@@ -208,11 +208,15 @@ class PPOTrainer:
                     action, logproba, _, value = self.agent.get_action_and_value(
                         next_obs, possible_moves=self.envs.mask_words)
                 m.values[step] = value.flatten()
-            if self.device_sampling:
-                action, logproba = self.envs.sample_policy(logits, zero_masked=True)
+            if self.device_sampling:  # the draw and the env step in one launch (bk_vec_step_policy)
+                action, logproba = self.envs.step_policy(logits, zero_masked=True)
+                obs, reward, term = self.envs.obs, self.envs.reward, self.envs.done.bool()
+            else:
+                obs, reward, term = None, None, None
             m.actions[step] = action
             m.logprobs[step] = logproba
-            obs, reward, term, _, _ = self.envs.step(action)
+            if not self.device_sampling:
+                obs, reward, term, _, _ = self.envs.step(action)
             m.rewards[step] = reward.view(-1)
             next_obs, next_done = obs.float(), term.float()
             self._ep_ret += reward

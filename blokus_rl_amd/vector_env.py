@@ -81,11 +81,24 @@ class BlokusVectorEnv:
                                           int(bool(zero_masked)), _ptr(self.actions), _ptr(self.logp), self._s()))
         return self.actions, self.logp
 
-    def step_policy(self, logits: torch.Tensor, zero_masked: bool = True):
-        """One rollout step on the device: sample_policy, then step_raw with its actions (two
-        launches, no host round trip). Returns (actions, logp) of the step."""
-        self.sample_policy(logits, zero_masked)
-        self.step_raw(self.actions)
+    def step_policy(self, logits: torch.Tensor, zero_masked: bool = True, fused: bool = True):
+        """One rollout step on the device: the policy draw and the env step in ONE launch
+        (bk_vec_step_policy: the draw reads the agent's legal mask from the step's own legality
+        pass); fused=False: sample_policy then step_raw (two launches, the same results bit for
+        bit). Returns (actions, logp) of the step; obs / mask_words / reward / done in place.
+        Capturable in a HIP graph."""
+        if not fused:
+            self.sample_policy(logits, zero_masked)
+            self.step_raw(self.actions)
+            return self.actions, self.logp
+        E, A = self.num_envs, self.eng.A
+        if not (logits.is_cuda and logits.device == torch.device(self.device) and logits.dtype == torch.float32
+                and logits.is_contiguous() and tuple(logits.shape) == (E, A)):
+            raise ValueError(f"step_policy wants contiguous float32 logits [{E}, {A}] on the env's device")
+        _check(self.eng.lib.bk_vec_step_policy(self.eng.h, _ptr(self.states), _ptr(self.rng), _ptr(logits),
+                                               int(bool(zero_masked)), E, _ptr(self.obs), _ptr(self.mask_words),
+                                               _ptr(self.reward), _ptr(self.done), _ptr(self.actions), _ptr(self.logp),
+                                               self._s()))
         return self.actions, self.logp
 
     def valid_mask(self) -> torch.Tensor:

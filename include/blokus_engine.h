@@ -247,9 +247,16 @@ int bk_vec_step(bk_ctx* ctx, void* states, uint64_t* rng, const int32_t* actions
  * reference's all -1e9 row). actions[e] is drawn from the softmax over the candidates by an
  * inverse CDF on the env's splitmix64 stream (one draw; rng[e] advanced), logp[e] =
  * logits[e][a] - logsumexp (Categorical.log_prob). Feed actions to bk_vec_step. 2-player 7x7
- * presets (<= 4096 ids). */
+ * presets (919 / 2522 ids). */
 int bk_vec_policy(bk_ctx* ctx, const float* logits, const uint64_t* mask, uint64_t* rng, int E, int zero_masked,
                   int32_t* actions, float* logp, void* stream);
+/* bk_vec_step_policy: one rollout step in one launch — the agent's id drawn from its policy
+ * logits exactly as bk_vec_policy draws it (same arithmetic, the legal mask taken from the step's
+ * own legality pass instead of HBM), written to actions / logp, then bk_vec_step with that id:
+ * the two launches' results bit for bit. The 2-player 7x7 presets. */
+int bk_vec_step_policy(bk_ctx* ctx, void* states, uint64_t* rng, const float* logits, int zero_masked, int E,
+                       uint8_t* obs, uint64_t* mask, float* reward, int32_t* done, int32_t* actions, float* logp,
+                       void* stream);
 
 /* ---------------------------------------------------------------- learner
  * Packed replay row (blokus_rl_amd/replay.py), fixed stride bk_replay_stride(cap), 16-B aligned:

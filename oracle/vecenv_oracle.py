@@ -3,10 +3,10 @@ the same rules (oracle/blokus_oracle.c) and the same per-env random stream as
 blokus_rl_amd/csrc/vecenv.hip, so the two compare bit for bit. The env restates blokus_gym
 `blokus-simple-v0` as the reference PPO uses it (ppo/trainer.py:128-175; docs/README.md:47-51).
 
-`policy_sample` restates k_vec_policy (the rollout's masked-policy draw, ppo/agent.py:27-42 +
-:148-156, ppo/trainer.py:144-155) in numpy float32 with the kernel's exact operation order: its
-exp / log polynomials, per-lane sums, the DPP scan order of BK_WAVE_SCAN and the inverse-CDF
-walk, so actions and log-probs compare bit for bit."""
+`policy_sample` restates policy_draw16 (the rollout's masked-policy draw of k_vec_policy and of
+the fused k_vec_step7, ppo/agent.py:27-42 + :148-156, ppo/trainer.py:144-155) in numpy float32 with
+the kernel's exact operation order: its exp / log polynomials, the per-lane sums, the 16-lane scan
+and the inverse-CDF walk, so actions and log-probs compare bit for bit."""
 from __future__ import annotations
 
 import numpy as np
@@ -57,84 +57,65 @@ def bk_logf(x):
     return (e.astype(F32) * F32(0.693147182) + (F32(2) * s) * q).astype(F32)
 
 
-def wave_scan_f32(s):
-    """common.h BK_WAVE_SCAN with op_add_f over the 64 lanes of s [..., 64]: row_shr 1/2/4/8 inside
-    each row of 16, then row_bcast:15 (rows 1 and 3 add lane 15 of the row below) and
-    row_bcast:31 (lanes >= 32 add lane 31)."""
+def scan16_f32(s):
+    """The 16-lane Hillis-Steele scan of policy_draw16 (DPP row_shr 1, 2, 4, 8) over s [..., 16]."""
     x = np.array(s, dtype=F32)
-    lane = np.arange(64)
+    lane = np.arange(16)
     for d in (1, 2, 4, 8):
         src = x.copy()
-        sel = (lane & 15) >= d
+        sel = lane >= d
         x[..., sel] = src[..., lane[sel] - d] + src[..., sel]
-    src = x.copy()
-    sel = (lane & 31) >= 16
-    x[..., sel] = src[..., (lane[sel] // 16) * 16 - 1] + src[..., sel]
-    src = x.copy()
-    sel = lane >= 32
-    x[..., sel] = src[..., 31:32] + src[..., sel]
     return x
 
 
 def policy_sample(logits, masks, rng, zero_masked: bool = True):
-    """k_vec_policy on the CPU. logits [E, A] f32, masks [E, W] u64 (the agent's legal ids), rng: E
-    int states. -> (actions int32 [E], logp f32 [E], new rng states). Per env: the candidates in
-    ascending id order are slots j = 0..K-1; lane l sums slots l, l + 64, ... in order."""
+    """policy_draw16 (vecenv.hip; k_vec_policy and the fused k_vec_step7 draw) on the CPU.
+    logits [E, A] f32, masks [E, W] u64 (the agent's legal ids), rng: E int states.
+    -> (actions int32 [E], logp f32 [E], new rng states). Lane j of an env owns mask words j, j + 16,
+    ...; its candidates in ascending id order."""
     logits = np.asarray(logits, dtype=F32)
     masks = np.asarray(masks, dtype=np.uint64)
     E, A = logits.shape
-    W = masks.shape[1]
     ids = np.arange(A)
-    bits = ((masks[:, ids // 64] >> (ids % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)  # [E, A]
+    lane_of = (ids // 64) % 16
+    bits = ((masks[:, ids // 64] >> (ids % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)
     cand = bits & ((logits != 0) if zero_masked else True)
     none = ~cand.any(axis=1)
     X = logits.copy()
     X[none] = F32(-1e9)
     cand[none] = True
     m = np.where(cand, X, F32(-np.inf)).max(axis=1).astype(F32)
-    K = cand.sum(axis=1)
-    Kmax = int(K.max())
-    nk = (Kmax + 63) // 64
-    slot_x = np.zeros((E, nk * 64), dtype=F32)
-    slot_id = np.zeros((E, nk * 64), dtype=np.int64)
-    used = np.arange(nk * 64)[None, :] < K[:, None]
-    order = np.argsort(~cand, axis=1, kind="stable")[:, :nk * 64] if nk * 64 <= A else None
-    if order is None:
-        order = np.argsort(~cand, axis=1, kind="stable")
-        order = np.pad(order, ((0, 0), (0, nk * 64 - A)))
-    slot_id[:] = order
-    slot_x[:] = np.take_along_axis(X, np.minimum(order, A - 1), axis=1)
-    P = np.where(used, bk_expf(np.where(used, slot_x - m[:, None], F32(0))), F32(0)).astype(F32)
-    P = P.reshape(E, nk, 64)
-    s = np.zeros((E, 64), dtype=F32)
-    for k in range(nk):
-        s = s + P[:, k, :]  # unused slots add +0
-    incl = wave_scan_f32(s)
-    S = incl[:, 63].copy()
+    P = np.where(cand, bk_expf(np.where(cand, X - m[:, None], F32(0))), F32(0)).astype(F32)
+    s = np.zeros((E, 16), dtype=F32)
+    for a in range(A):  # each lane's sum in ascending id order
+        j = lane_of[a]
+        s[:, j] = np.where(cand[:, a], s[:, j] + P[:, a], s[:, j])
+    incl = scan16_f32(s)
+    S = incl[:, 15].copy()
     z = [mix64(int(st)) for st in rng]
     new_rng = [(int(st) + GOLDEN) & M64 for st in rng]
     u = np.array([zz >> 40 for zz in z], dtype=np.uint32).astype(F32) * F32(2.0 ** -24)
     target = (S * u).astype(F32)
     over = incl > target[:, None]
     pos = s > F32(0)
-    last_pos = np.where(pos.any(1), 63 - pos[:, ::-1].argmax(1), 0)
+    last_pos = np.where(pos.any(1), 15 - pos[:, ::-1].argmax(1), 0)
     sel = np.where(over.any(1), over.argmax(1), last_pos)
     er = np.arange(E)
     acc = np.where(sel > 0, incl[er, np.maximum(sel - 1, 0)], F32(0)).astype(F32)
     pick = np.full(E, -1)
     last = np.full(E, -1)
-    for k in range(nk):
-        pt = P[er, k, sel]
-        ok = (pt > F32(0)) & (pick < 0)
-        acc = np.where(ok, acc + pt, acc).astype(F32)
-        last = np.where(ok, 64 * k + sel, last)
-        pick = np.where(ok & (acc > target), 64 * k + sel, pick)
+    for a in range(A):  # the selected lane's walk, ids ascending
+        live = (lane_of[a] == sel) & cand[:, a] & (pick < 0)
+        pa = P[:, a]
+        ok = live & (pa > F32(0))
+        acc = np.where(ok, acc + pa, acc).astype(F32)
+        last = np.where(ok, a, last)
+        pick = np.where(ok & (acc > target), a, pick)
     pick = np.where(pick < 0, last, pick)
     good = pick >= 0
     pk = np.maximum(pick, 0)
-    actions = np.where(good, slot_id[er, pk], A).astype(np.int32)
-    xa = slot_x[er, pk]
-    logp = np.where(good, xa - (m + bk_logf(np.maximum(S, F32(1)))), F32(np.nan)).astype(F32)
+    actions = np.where(good, pk, A).astype(np.int32)
+    logp = np.where(good, X[er, pk] - (m + bk_logf(np.maximum(S, F32(1)))), F32(np.nan)).astype(F32)
     return actions, logp, new_rng
 
 

@@ -8,7 +8,7 @@ import numpy as np
 import torch
 from scipy import stats
 
-from oracle.vecenv_oracle import bk_expf, bk_logf, policy_sample, wave_scan_f32
+from oracle.vecenv_oracle import bk_expf, bk_logf, policy_sample, scan16_f32
 
 
 def _mask_of(ids, W=15):
@@ -34,8 +34,8 @@ def test_exp_log_accuracy():
     assert bk_expf(np.float32(0)) == 1.0 and bk_expf(np.float32(-81)) == 0.0
     y = np.linspace(1, 5000, 100001).astype(np.float32)
     assert np.max(np.abs(bk_logf(y) - np.log(y.astype(np.float64))) / np.maximum(np.log(y), 1e-3)) < 1e-6
-    s = np.random.default_rng(0).random((4, 64)).astype(np.float32)
-    np.testing.assert_allclose(wave_scan_f32(s), np.cumsum(s, axis=1), rtol=1e-6)
+    s = np.random.default_rng(0).random((4, 16)).astype(np.float32)
+    np.testing.assert_allclose(scan16_f32(s), np.cumsum(s, axis=1), rtol=1e-6)
 
 
 def test_policy_sample_law_and_logprob():

@@ -200,7 +200,16 @@ def test_ppo_rollout_draws(device_sampling):
         rows.append(logits.clone())
         return orig_sample(logits, zero_masked)
 
-    tr.envs.step, tr.envs.sample_policy = rec_step, rec_sample
+    orig_sp = tr.envs.step_policy
+
+    def rec_step_policy(logits, zero_masked=True):
+        masks.append(tr.envs.valid_mask().clone())
+        rows.append(logits.clone())
+        a, lp = orig_sp(logits, zero_masked)
+        acts.append(a.long().clone())
+        return a, lp
+
+    tr.envs.step, tr.envs.sample_policy, tr.envs.step_policy = rec_step, rec_sample, rec_step_policy
     tr._play_env(obs.float(), torch.zeros(64, device=tr.device))
     assert len(acts) == hp.num_steps
     illegal = 0

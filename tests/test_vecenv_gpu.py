@@ -276,3 +276,25 @@ def test_policy_sample_law_and_logprob_vs_torch():
     zero_ids = set(lid[::4].tolist())
     hits = sum(1 for v in a.cpu().tolist() if v in zero_ids)
     assert hits > 0
+
+
+@pytest.mark.parametrize("max_cells,E", [(4, 37), (5, 21)])
+def test_fused_policy_step_matches_two_launches(max_cells, E):
+    """bk_vec_step_policy (the draw inside k_vec_step7) against bk_vec_policy + bk_vec_step on a
+    twin env: actions, log-probs, states, observations, masks, rewards, dones and random streams
+    bit for bit every step, zero_masked on and off, with all-zero (no-candidate) rows."""
+    from blokus_rl_amd.vector_env import BlokusVectorEnv
+
+    env1, env2 = BlokusVectorEnv(E, 7, max_cells), BlokusVectorEnv(E, 7, max_cells)
+    A = env1.eng.A
+    env1.reset(seed=7)
+    env2.reset(seed=7)
+    rng = np.random.default_rng(3)
+    for t in range(30):
+        zm = t % 5 != 4
+        x = torch.from_numpy(_policy_logits(E, A, t, rng)).to(env1.device)
+        a1, l1 = env1.step_policy(x, zero_masked=zm)
+        a2, l2 = env2.step_policy(x, zero_masked=zm, fused=False)
+        assert torch.equal(a1, a2) and torch.equal(l1.view(torch.int32), l2.view(torch.int32)), t
+        for n in ("states", "obs", "mask_words", "rng", "reward", "done"):
+            assert torch.equal(getattr(env1, n), getattr(env2, n)), (t, n)

@@ -21,5 +21,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL $lim rocprofv3 --pmc $grp --kernel-trace -d $dir/p$i -o c --output-format csv -- "$@" \
     > $dir/p$i.log 2>&1 || { echo "FAILED $key pass $i"; tail -5 $dir/p$i.log; exit 1; }
 done
-python tools/pmc_to_json.py $out $key $pat $units $algo "$note" $dir/p* || exit 1
+python tools/pmc_to_json.py "$out" "$key" "$pat" "$units" "$algo" "$note" $dir/p* || exit 1
 rm -rf $dir/p?   # keep the logs only (per-dispatch CSVs can exceed gpurun's return size)

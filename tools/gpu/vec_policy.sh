@@ -16,7 +16,10 @@ cat gpurun_out/r06_vec_bench.json
 tools/gpu/pmc_kernel.sh gpurun_out/r06_pmc_vec_step7.json k_vec_step7 k_vec_step7 8192 3219456 \
   "round 6: rocprofv3 --pmc passes of tools/vec_pmc.py random (eager k_vec_step7, in-kernel agent draws, 8192 envs, 70 launches); algorithmic bytes = 8192 x 393" \
   120 -- python tools/vec_pmc.py random 50 || exit 1
-tools/gpu/pmc_kernel.sh gpurun_out/r06_pmc_vec_policy.json k_vec_policy k_vec_policy 8192 31293440 \
-  "round 6: rocprofv3 --pmc passes of tools/vec_pmc.py policy (eager bk_vec_policy, 8192 envs x 919 ids, 70 launches); algorithmic bytes = 8192 x (919 x 4 logits + 15 x 8 mask + 16 rng + 8 out)" \
+tools/gpu/pmc_kernel.sh gpurun_out/r06_pmc_vec_policy.json k_vec_step7_policy "k_vec_step7<4, 16, 2>|k_vec_step7ILi4ELi16ELi2E" 8192 0 \
+  "round 6: rocprofv3 --pmc passes of tools/vec_pmc.py policy (eager fused draw + step, k_vec_step7<4,16,2>, 8192 envs, 70 launches); algorithmic bytes per env: 393 + 4 x the legal ids + 8 (the bench line's bytes_per_unit)" \
   120 -- python tools/vec_pmc.py policy 50 || exit 1
+tools/gpu/pmc_kernel.sh gpurun_out/r06_pmc_vec_draw.json k_vec_policy k_vec_policy 8192 0 \
+  "round 6: rocprofv3 --pmc passes of tools/vec_pmc.py draw (eager standalone k_vec_policy, 16 lanes per env, 8192 envs, 70 launches); algorithmic bytes per env: 4 x the legal ids + 120 mask + 16 rng + 8 out (the bench line's draw_alone.bytes_per_unit)" \
+  120 -- python tools/vec_pmc.py draw 50 || exit 1
 echo ALLOK

@@ -1,7 +1,7 @@
 """Config-5 kernels for a rocprofv3 PMC pass (tools/gpu/pmc_kernel.sh): eager launches of one
 mode at the benchmark size, after a warm-up. mode: random (k_vec_step7 with in-kernel agent
-draws: the bench headline's kernel) or policy (bk_vec_policy + k_vec_step7 with the drawn ids,
-random [E, A] logits resident in HBM).  usage: python tools/vec_pmc.py <mode> [steps] [envs]"""
+draws: the bench headline's kernel), policy (the fused draw + step, k_vec_step7<4, 16, 2>, random
+[E, A] logits resident in HBM) or draw (the standalone k_vec_policy, then the step with its ids).  usage: python tools/vec_pmc.py <mode> [steps] [envs]"""
 import os
 import sys
 
@@ -19,7 +19,9 @@ logits = (torch.randn((E, env.eng.A), device=env.device) * 2.0).contiguous()
 for i in range(20 + steps):
     if mode == "random":
         env.step_raw(None)
-    else:
+    elif mode == "policy":
         env.step_policy(logits)
+    else:
+        env.step_policy(logits, fused=False)
 torch.cuda.synchronize()
 print(mode, steps, "steps ok")
