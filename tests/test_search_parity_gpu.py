@@ -4,8 +4,9 @@ softmax + expand/backup + the next descent}) on 64 trees of 20x20 boards with a 
 replayed tree by tree through the CPU restatement of the reference search (oracle MCTSOracle,
 mcts.py:7-99) with the GPU's own leaf evaluations handed over as is (prior_mode 1 semantics:
 the float32 priors the search stored, the float32 values the net returned). Every expanded
-node's N and Q (float64) and the root pi must agree bit for bit; the stored priors must equal a
-torch fp32 policy head over the same features to 1e-5.
+node's N and Q (float64) and the root pi must agree bit for bit; the stored priors of EVERY
+expanded node must equal an fp64 masked softmax of the policy head over the same features to
+1e-5 (the oracle is handed the stored priors, so this is the independent check on them).
 
 Leaf values are recomputed by the same net on each node's observation in 64-row batches (the
 x3 kernel's rows do not depend on the batch, tests/test_leafnet_gpu.py); the priors are read
@@ -62,6 +63,19 @@ def _dump_forest(sp, eng, o, starts):
     return trees
 
 
+def _check_priors(ev, nodes, feats):
+    """Every expanded node's stored priors = the policy head's masked softmax over its legal ids,
+    recomputed in float64 from the node's policy features: nodes {key: (state, ids, N, Q, P)},
+    feats {key: features}."""
+    W = ev.policy_w.cpu().double().numpy()
+    b = ev.policy_b.cpu().double().numpy()
+    assert nodes and set(nodes) <= set(feats)
+    for key, (_, ids, _, _, P) in nodes.items():
+        lg = W[ids] @ feats[key].astype(np.float64) + b[ids]
+        e = np.exp(lg - lg.max())
+        np.testing.assert_allclose(P, e / e.sum(), rtol=1e-5, atol=1e-7, err_msg=str(key))
+
+
 def test_config3_search_matches_oracle_replay():
     from blokus_rl_amd.alphazero.selfplay import SelfPlay
     from blokus_rl_amd.boards import random_boards
@@ -98,14 +112,8 @@ def test_config3_search_matches_oracle_replay():
         for j, key in enumerate(chunk):
             vals[key], feats[key] = v[j].astype(np.float64), pf[j]
 
-    # the stored priors are the policy head's masked softmax over the legal ids
-    W = ev.policy_w.cpu().double().numpy()
-    b = ev.policy_b.cpu().double().numpy()
-    for t in range(0, T, 9):
-        s, ids, _, _, P = trees[t][o.hash(roots_h[t])]
-        lg = W[ids] @ feats[(t, o.hash(roots_h[t]))].astype(np.float64) + b[ids]
-        e = np.exp(lg - lg.max())
-        np.testing.assert_allclose(P, e / e.sum(), rtol=1e-5, atol=1e-7)
+    # the stored priors of every expanded node are the policy head's masked softmax
+    _check_priors(ev, {(t, h): nd for t in range(T) for h, nd in trees[t].items()}, feats)
 
     for t in range(T):
         nodes = trees[t]
@@ -168,16 +176,17 @@ def test_config3_tree_reuse_matches_oracle_replay():
 
     ev = sp.evaluator
     keys = [(t, h) for t in range(T) for h in final[t]]
-    vals = {}
+    vals, feats = {}, {}
     for i in range(0, len(keys), T):
         chunk = keys[i:i + T]
         st = np.zeros((T, roots[0].shape[1]), dtype=np.uint8)
         for j, (t, h) in enumerate(chunk):
             st[j] = final[t][h][0]
-        _, v = ev._forward(eng.observe(torch.from_numpy(st).to(eng.device)))
-        v = v.cpu().numpy()
+        pf, v = ev._forward(eng.observe(torch.from_numpy(st).to(eng.device)))
+        v, pf = v.cpu().numpy(), pf.cpu().numpy()
         for j, key in enumerate(chunk):
-            vals[key] = v[j].astype(np.float64)
+            vals[key], feats[key] = v[j].astype(np.float64), pf[j]
+    _check_priors(ev, {(t, h): final[t][h] for t, h in keys}, feats)
 
     for t in range(T):
         nodes = final[t]
@@ -279,22 +288,23 @@ def test_config3_game_turnover_matches_oracle_replay():
     assert ended >= 16 and len(restarted) >= 8, (ended, len(restarted))
 
     # leaf values of every node, recomputed by the same net (a value depends on the state only)
-    vals, states = {}, {}
+    vals, feats, states = {}, {}, {}
     for p in plies:
         for tr in p[2]:
             for h, nd in tr.items():
-                states.setdefault(h, nd[0])
+                states.setdefault(h, nd)
     hs = list(states)
     ev = sp.evaluator
     for j in range(0, len(hs), T):
         chunk = hs[j:j + T]
         st = np.zeros((T, init.shape[0]), dtype=np.uint8)
         for r, h in enumerate(chunk):
-            st[r] = states[h]
-        _, v = ev._forward(eng.observe(torch.from_numpy(st).to(eng.device)))
-        v = v.cpu().numpy()
+            st[r] = states[h][0]
+        pf, v = ev._forward(eng.observe(torch.from_numpy(st).to(eng.device)))
+        v, pf = v.cpu().numpy(), pf.cpu().numpy()
         for r, h in enumerate(chunk):
-            vals[h] = v[r].astype(np.float64)
+            vals[h], feats[h] = v[r].astype(np.float64), pf[r]
+    _check_priors(ev, states, feats)
 
     for t in range(T):
         cur = {}
