@@ -88,7 +88,8 @@ __device__ __forceinline__ void orient_step(const DevPreset& dp, const RowCtx& c
   }
   const uint32_t colmask = (1u << W) - 1u;  // wave-uniform
   const uint32_t pmask = (uint32_t)__builtin_amdgcn_sbfe((int)c.pieces, oc.piece, 1);
-  const uint32_t v = __brev(good & ~bad) & colmask & c.rowok[oc.h] & pmask;
+  // SKIP0 (one board per wave, row_ctx): rows past the board are forbidden in fr, no row mask
+  const uint32_t v = __brev(good & ~bad) & colmask & (SKIP0 ? ~0u : c.rowok[oc.h]) & pmask;
   const int bit = base + c.rN1 - c.r * oc.w;
   const uint64_t x = (uint64_t)v << (bit & 31);
   uint32_t* dst = c.mb + (bit >> 5);
@@ -184,7 +185,7 @@ __device__ __forceinline__ void orient_dispatch_nt(const DevPreset& dp, const Ro
 }
 
 // The row context of colour q on the board s (LDS) for lanes 0..N-1 (the board's rows); lanes
-// past N and rows past the board are masked by rowok. first: q has no cell yet. (The lean step on
+// past N (rows past the board) are all forbidden. first: q has no cell yet. (The lean step on
 // board-order rows here measured 0.3% slower end to end: the search's bitmasks skip used pieces
 // and zero fields, so their VALU is not on the step's critical path.)
 __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s, int q, uint32_t* m32) {
@@ -206,7 +207,11 @@ __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
   RowCtx c;
-  c.fr[0] = __brev(forb);
+  // the lanes past the board (rows >= N) are all forbidden: a placement reaching below the board
+  // then has a forbidden cell in every origin column < W (its bottom row's cell), so the single-
+  // board steps (SKIP0, orient_any) need no per-height row mask — six fewer live registers in the
+  // search's descent, which spilled them to scratch (a vmcnt(0) reload per orientation tested)
+  c.fr[0] = ok ? __brev(forb) : ~0u;
   c.ar[0] = __brev(anch);
 #pragma unroll
   for (int d = 1; d < 5; ++d) {
@@ -219,7 +224,7 @@ __device__ __forceinline__ RowCtx row_ctx(const DevPreset& dp, const uint32_t* s
   c.pieces = s[kWPieces + q];
   c.upieces = __builtin_amdgcn_readfirstlane(c.pieces);
 #pragma unroll
-  for (int h = 0; h < 6; ++h) c.rowok[h] = (ok && r + h <= N) ? ~0u : 0u;
+  for (int h = 0; h < 6; ++h) c.rowok[h] = ~0u;  // unused by the single-board steps (above)
   c.mb = m32;
   return c;
 }
@@ -242,7 +247,7 @@ __device__ __forceinline__ bool orient_any(const DevPreset& dp, const RowCtx& c,
       good |= c.ar[oc.dr[k]] << oc.dc[k];
     }
     const uint32_t colmask = (1u << (dp.N - oc.w + 1)) - 1u;
-    const uint32_t v = __brev(good & ~bad) & colmask & c.rowok[oc.h];
+    const uint32_t v = __brev(good & ~bad) & colmask;  // rows past the board: forbidden in fr (row_ctx)
     found = __ballot(v != 0u) != 0ull;
   };
   (step(std::integral_constant<int, (int)Os>{}), ...);
@@ -363,7 +368,9 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
       anch = (up << 1 | up >> 1 | dn << 1 | dn >> 1) & dp.full_row;
   }
   RowCtx c;
-  c.fr[0] = __brev(forb);
+  // rows past the board (and idle lanes) forbidden, as row_ctx: the single-board step form
+  // (SKIP0, the WPB > 1 variants' orient_step_at) relies on it instead of rowok
+  c.fr[0] = ok ? __brev(forb) : ~0u;
   c.ar[0] = __brev(anch);
   if constexpr (SPLIT == 3) {
     c.fr[0] = ok ? (forb | ~dp.full_row) : ~0u;
@@ -374,7 +381,7 @@ __global__ __launch_bounds__(64 * WPB) void k_legal_mask_rows(DevPreset dp, cons
     const int src = l + d > kWave - 1 ? kWave - 1 : l + d;
     c.fr[d] = __shfl(c.fr[0], src, kWave);
     c.ar[d] = __shfl(c.ar[0], src, kWave);
-    if constexpr (SPLIT == 3) c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;
+    c.fr[d] = (ok && r + d < N) ? c.fr[d] : ~0u;  // the next board's rows are past this board
   }
   c.r = r;
   c.rN1 = r * (N + 1);

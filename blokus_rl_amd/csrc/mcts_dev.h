@@ -1015,8 +1015,6 @@ __device__ __forceinline__ void mask_slices_claim(const DevPreset& dp, const uin
     // compiler would otherwise keep every slice's shifted rows live at once)
 #pragma unroll
     for (int d = 0; d < 5; ++d) asm volatile("" : "+v"(c.fr[d]), "+v"(c.ar[d]));
-#pragma unroll
-    for (int h = 0; h < 6; ++h) asm volatile("" : "+v"(c.rowok[h]));
     asm volatile("" : "+v"(c.r), "+v"(c.rN1), "+v"(c.pieces));
     int k = 0;
     if (lane_id() == 0) k = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
