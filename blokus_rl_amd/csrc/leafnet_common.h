@@ -15,6 +15,10 @@ using f32x2 = float __attribute__((ext_vector_type(2)));
 using u32x4 = unsigned __attribute__((ext_vector_type(4)));
 using u32x2 = unsigned __attribute__((ext_vector_type(2)));
 
+#ifndef BK_LN_DUMMY
+#define BK_LN_DUMMY 0  // timing diagnostic only: dummy VALU ops after each MFMA triple (ln_chunk;
+                       // profiles/r06_leafnet_valu_shadow.json: ~5.5 cycles each, not hidden)
+#endif
 #ifndef BK_LN_STAMP
 #define BK_LN_STAMP 0  // timing diagnostics only: per-wave s_memtime stamps (bk_ln_stamps)
 #endif
@@ -253,6 +257,19 @@ __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, c
           "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
           : BK_ACC_RW(acc[g])
           : "v"(ah), "v"(bh), "v"(al), "v"(bl));
+#if BK_LN_DUMMY
+    {  // timing diagnostic only: BK_LN_DUMMY independent VALU ops after each triple (the MFMA shadow)
+      float d0 = __builtin_bit_cast(float, (unsigned)g), d1 = d0;
+#pragma unroll
+      for (int k = 0; k < BK_LN_DUMMY; ++k) {
+        if (k & 1)
+          asm volatile("v_add_f32 %0, %0, %0" : "+v"(d1));
+        else
+          asm volatile("v_add_f32 %0, %0, %0" : "+v"(d0));
+      }
+      asm volatile("" ::"v"(d0), "v"(d1));
+    }
+#endif
   }
 }
 

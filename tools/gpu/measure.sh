@@ -51,5 +51,9 @@ python tools/pmc_to_json.py gpurun_out/r06_pmc_learner.json k_bn_axpb k_bn_axpb 
   "round 6: same passes: the mean over every k_bn_axpb dispatch (forward y = x s + t: 209,715,200 B; backward dx = dy k1 + k2 + x k3: 314,572,800 B; as many of each)" /tmp/pmc_ln/p* || exit 1
 BK_PMC_SCALE=2 python tools/pmc_to_json.py gpurun_out/r06_pmc_learner.json "k_policy_loss+grad" k_policy_loss 1024 0 \
   "round 6: same passes: 2 x the mean over the k_policy_loss and k_policy_loss_grad dispatches = one launch pair; algorithmic bytes per pair: the bench line's bytes_per_launch_pair (K-dependent)" /tmp/pmc_ln/p* || exit 1
+for k in k_splin_fwd k_splin_dx k_splin_dw; do
+  python tools/pmc_to_json.py gpurun_out/r06_pmc_learner.json $k "$k(?!_)" 1024 0 \
+    "round 6: same passes: every $k dispatch (the learner's policy Linear at the batch's legal ids, trainfc.hip); algorithmic bytes K-dependent (a 3.2-KB W or pf row per (row, legal id) pair from the Infinity Cache / L2, DESIGN section 4), so only the measured traffic is given" /tmp/pmc_ln/p* || exit 1
+done
 rm -rf /tmp/pmc_ln
 echo ALLOK
