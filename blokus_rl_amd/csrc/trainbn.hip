@@ -17,7 +17,8 @@ constexpr int kBnGrid = 512;
 constexpr int kBnAxGrid = 2048;  // k_bn_axpb's workgroups (grid-stride)
 
 // per workgroup: sum over its rows of a[r][c] (and of a[r][c] * (b[r][c] - mb[c]) when b != null,
-// else of a[r][c]^2) in fp64 -> part[g][c][2]
+// else of a[r][c]^2) in fp64 -> part[c][g][2] (channel-major: each finalize workgroup then reads
+// its channel's G partials contiguously)
 // (rp, rq non-null, the fused ReLU's backward: a counts only where b rp + rq > 0, i.e. where the
 // forward's batch-norm output was positive)
 __global__ __launch_bounds__(kBnThreads) void k_bn_reduce(const float* __restrict__ a, const float* __restrict__ b,
@@ -72,21 +73,23 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_reduce(const float* __restric
     double acc = 0;
 #pragma unroll
     for (int i = 0; i < kBnRows; ++i) acc += red[i][c][k];
-    part[((size_t)blockIdx.x * 64 + c) * 2 + k] = acc;
+    part[((size_t)c * gridDim.x + blockIdx.x) * 2 + k] = acc;
   }
 }
 
-// the per-workgroup partial sums part[g][c][2] added over g for channel c = blockIdx.x (one
-// workgroup per channel: 256 threads each take g = tid, tid + 256, ... in order, then a fixed
-// LDS tree); every thread gets the channel's two totals
+// the per-workgroup partial sums part[c][g][NV] (NV = 2 values, or 1: the second sum is 0) added
+// over g for channel c = blockIdx.x (one workgroup per channel: 256 threads each take g = tid,
+// tid + 256, ... in order, then a fixed LDS tree); every thread gets the channel's two totals
 constexpr int kBnFinThreads = 256;
+template <int NV = 2>
 __device__ __forceinline__ void bn_sum_parts(const double* __restrict__ part, int G, double& s0, double& s1) {
   __shared__ double red[kBnFinThreads][2];
   const int c = blockIdx.x, t = threadIdx.x;
   double a = 0, b = 0;
+  const double* pc = part + (size_t)c * G * NV;
   for (int g = t; g < G; g += kBnFinThreads) {
-    a += part[((size_t)g * 64 + c) * 2];
-    b += part[((size_t)g * 64 + c) * 2 + 1];
+    a += pc[(size_t)g * NV];
+    if (NV == 2) b += pc[(size_t)g * NV + 1];
   }
   red[t][0] = a;
   red[t][1] = b;
@@ -147,8 +150,8 @@ __global__ __launch_bounds__(kBnFinThreads) void k_bn_finalize_bwd(const double*
 // out = a * p[c] + q[c] (+ b * r[c]) over [M][64] (forward: y = x scale + shift; backward:
 // dx = dy k1 + k2 + x k3). relu: out = max(out, 0) (the fused ReLU of the forward). mp / mq
 // non-null (the fused ReLU's backward): a counts only where b mp + mq > 0. colsum non-null: the
-// workgroup's per-channel sums of out in fp64 -> colsum[g][c][0] (the bias gradient of the conv
-// that feeds the batch norm, k_colsum_finalize adds them up in a fixed order).
+// workgroup's per-channel sums of out in fp64 -> colsum[c][g] (the bias gradient of the conv that
+// feeds the batch norm, k_colsum_finalize adds them up in a fixed order).
 __global__ __launch_bounds__(256) void k_bn_axpb(const float* __restrict__ a, const float* __restrict__ b,
                                                  const float* __restrict__ p, const float* __restrict__ q,
                                                  const float* __restrict__ rr, int64_t n4, float* __restrict__ out,
@@ -202,17 +205,16 @@ __global__ __launch_bounds__(256) void k_bn_axpb(const float* __restrict__ a, co
       double acc = 0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc += red[i][threadIdx.x];
-      colsum[((size_t)blockIdx.x * 64 + threadIdx.x) * 2] = acc;
-      colsum[((size_t)blockIdx.x * 64 + threadIdx.x) * 2 + 1] = 0.0;
+      colsum[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = acc;
     }
   }
 }
 
-// colsum partials [G][64][2] -> out[c] (f32), in bn_sum_parts' fixed order (64 workgroups)
+// colsum partials [64][G] -> out[c] (f32), in bn_sum_parts' fixed order (64 workgroups)
 __global__ __launch_bounds__(kBnFinThreads) void k_colsum_finalize(const double* __restrict__ part, int G,
                                                                    float* __restrict__ outc) {
   double s0, s1;
-  bn_sum_parts(part, G, s0, s1);
+  bn_sum_parts<1>(part, G, s0, s1);
   if (threadIdx.x == 0) outc[blockIdx.x] = (float)s0;
 }
 
