@@ -253,8 +253,8 @@ class SparsePolicyLinear(torch.autograd.Function):
         B, F = pf.shape
         cap = ids.shape[1]
         xs = torch.empty((B, cap), dtype=torch.float32, device=pf.device)
-        _check(lib.bk_sparse_linear_fwd(_ptr(pf), B, F, _ptr(W.detach()), _ptr(bias.detach()), _ptr(ids), _ptr(k), cap,
-                                        _ptr(xs), _stream(pf.device)))
+        _check(lib.bk_sparse_linear_fwd(_ptr(pf), B, F, _ptr(W.detach()), _ptr(bias.detach()), W.shape[0], _ptr(ids),
+                                        _ptr(k), cap, _ptr(xs), _stream(pf.device)))
         ctx.save_for_backward(pf, W, ids, k)
         return xs
 
@@ -270,7 +270,7 @@ class SparsePolicyLinear(torch.autograd.Function):
         dpf = dW = db = None
         if ctx.needs_input_grad[0]:
             dpf = torch.empty_like(pf)
-            _check(lib.bk_sparse_linear_dx(_ptr(g), B, F, _ptr(W.detach()), _ptr(ids), _ptr(k), cap, _ptr(dpf), st))
+            _check(lib.bk_sparse_linear_dx(_ptr(g), B, F, _ptr(W.detach()), A, _ptr(ids), _ptr(k), cap, _ptr(dpf), st))
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             count = torch.zeros(A, dtype=torch.int32, device=dev)
             _check(lib.bk_sparse_linear_index(_ptr(ids), _ptr(k), cap, B, A, _ptr(count), None, None, None, st))

@@ -32,9 +32,13 @@ __device__ __forceinline__ float fc_wave_sum(float x) {
   return readlane_f(x, kWave - 1);
 }
 
+// an id outside [0, A) (not a legal id of the table) contributes nothing: its logit is 0 and it
+// enters no gradient (the loads stay inside W)
+__device__ __forceinline__ bool fc_id_ok(int a, int A) { return a < A; }
+
 __global__ __launch_bounds__(256) void k_splin_fwd(const float* __restrict__ pf, int F4, const float* __restrict__ W,
                                                    const float* __restrict__ bias, const int16_t* __restrict__ ids,
-                                                   const int32_t* __restrict__ kk, int cap, float* __restrict__ xs) {
+                                                   const int32_t* __restrict__ kk, int cap, int A, float* __restrict__ xs) {
   const int b = blockIdx.x, w = threadIdx.x >> 6, l = lane_id();
   const int K = fc_clamp_k(kk[b], cap);
   const f32x4* p4 = reinterpret_cast<const f32x4*>(pf) + (size_t)b * F4;
@@ -49,7 +53,9 @@ __global__ __launch_bounds__(256) void k_splin_fwd(const float* __restrict__ pf,
   // two ids per wave in flight
   for (int j = w; j < K; j += 8) {
     const int j2 = j + 4;
-    const int a0 = (uint16_t)ir[j], a1 = j2 < K ? (uint16_t)ir[j2] : a0;
+    const int i0 = (uint16_t)ir[j], i1 = j2 < K ? (uint16_t)ir[j2] : i0;
+    const bool ok0 = fc_id_ok(i0, A), ok1 = fc_id_ok(i1, A);
+    const int a0 = ok0 ? i0 : 0, a1 = ok1 ? i1 : 0;
     const f32x4* r0 = reinterpret_cast<const f32x4*>(W) + (size_t)a0 * F4;
     const f32x4* r1 = reinterpret_cast<const f32x4*>(W) + (size_t)a1 * F4;
     f32x4 w0[kFcSlots], w1[kFcSlots];
@@ -68,8 +74,8 @@ __global__ __launch_bounds__(256) void k_splin_fwd(const float* __restrict__ pf,
     s0 = fc_wave_sum(s0);
     s1 = fc_wave_sum(s1);
     if (l == 0) {
-      xr[j] = s0 + bias[a0];
-      if (j2 < K) xr[j2] = s1 + bias[a1];
+      xr[j] = ok0 ? s0 + bias[a0] : 0.f;
+      if (j2 < K) xr[j2] = ok1 ? s1 + bias[a1] : 0.f;
     }
   }
   for (int j = K + threadIdx.x; j < cap; j += 256) xr[j] = 0.f;
@@ -77,7 +83,7 @@ __global__ __launch_bounds__(256) void k_splin_fwd(const float* __restrict__ pf,
 
 __global__ __launch_bounds__(256) void k_splin_dx(const float* __restrict__ g, int F4, const float* __restrict__ W,
                                                   const int16_t* __restrict__ ids, const int32_t* __restrict__ kk,
-                                                  int cap, float* __restrict__ dpf) {
+                                                  int cap, int A, float* __restrict__ dpf) {
   __shared__ f32x4 part[4][kFcMaxF4];
   const int b = blockIdx.x, w = threadIdx.x >> 6, l = lane_id();
   const int K = fc_clamp_k(kk[b], cap);
@@ -88,8 +94,10 @@ __global__ __launch_bounds__(256) void k_splin_dx(const float* __restrict__ g, i
   for (int s = 0; s < kFcSlots; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int j = w; j < K; j += 8) {
     const int j2 = j + 4;
-    const int a0 = (uint16_t)ir[j], a1 = j2 < K ? (uint16_t)ir[j2] : a0;
-    const float g0 = gr[j], g1 = j2 < K ? gr[j2] : 0.f;
+    const int i0 = (uint16_t)ir[j], i1 = j2 < K ? (uint16_t)ir[j2] : i0;
+    const bool ok0 = fc_id_ok(i0, A), ok1 = fc_id_ok(i1, A);
+    const int a0 = ok0 ? i0 : 0, a1 = ok1 ? i1 : 0;
+    const float g0 = ok0 ? gr[j] : 0.f, g1 = (j2 < K && ok1) ? gr[j2] : 0.f;
     const f32x4* r0 = reinterpret_cast<const f32x4*>(W) + (size_t)a0 * F4;
     const f32x4* r1 = reinterpret_cast<const f32x4*>(W) + (size_t)a1 * F4;
     f32x4 w0[kFcSlots], w1[kFcSlots];
@@ -115,21 +123,22 @@ __global__ __launch_bounds__(256) void k_splin_dx(const float* __restrict__ g, i
 // the (id -> pairs) index: count[a] (atomics), then slots via an exclusive scan on the host side
 // (torch.cumsum) and k_splin_fill's atomic cursors; the order inside an id is fixed in k_splin_dw
 __global__ __launch_bounds__(256) void k_splin_count(const int16_t* __restrict__ ids, const int32_t* __restrict__ kk,
-                                                     int cap, int B, int32_t* __restrict__ count) {
+                                                     int cap, int B, int A, int32_t* __restrict__ count) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)B * cap) return;
   const int b = (int)(i / cap), j = (int)(i - (int64_t)b * cap);
-  if (j < fc_clamp_k(kk[b], cap)) atomicAdd(count + (uint16_t)ids[i], 1);
+  const int a = (uint16_t)ids[i];
+  if (j < fc_clamp_k(kk[b], cap) && fc_id_ok(a, A)) atomicAdd(count + a, 1);
 }
 
 __global__ __launch_bounds__(256) void k_splin_fill(const int16_t* __restrict__ ids, const int32_t* __restrict__ kk,
-                                                    int cap, int B, const int32_t* __restrict__ start,
+                                                    int cap, int B, int A, const int32_t* __restrict__ start,
                                                     int32_t* __restrict__ cursor, int32_t* __restrict__ pairs) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)B * cap) return;
   const int b = (int)(i / cap), j = (int)(i - (int64_t)b * cap);
-  if (j < fc_clamp_k(kk[b], cap)) {
-    const int a = (uint16_t)ids[i];
+  const int a = (uint16_t)ids[i];
+  if (j < fc_clamp_k(kk[b], cap) && fc_id_ok(a, A)) {
     pairs[start[a] + atomicAdd(cursor + a, 1)] = (int32_t)i;
   }
 }
@@ -197,23 +206,23 @@ using namespace bk;
 
 extern "C" {
 
-int bk_sparse_linear_fwd(const float* pf, int B, int F, const float* W, const float* bias, const int16_t* ids,
+int bk_sparse_linear_fwd(const float* pf, int B, int F, const float* W, const float* bias, int A, const int16_t* ids,
                          const int32_t* k, int cap, float* xs, void* stream) {
-  BK_REQUIRE(pf && W && bias && ids && k && xs && B >= 0 && cap > 0, "bad argument");
+  BK_REQUIRE(pf && W && bias && ids && k && xs && B >= 0 && cap > 0 && A > 0, "bad argument");
   BK_REQUIRE(F > 0 && F % 4 == 0 && F / 4 <= kFcMaxF4, "bk_sparse_linear: F a multiple of 4, <= 1024");
   BK_REQUIRE(((uintptr_t)pf & 15u) == 0 && ((uintptr_t)W & 15u) == 0, "bk_sparse_linear: 16-byte aligned pf / W");
   if (B == 0) return BK_OK;
-  hipLaunchKernelGGL(k_splin_fwd, dim3(B), dim3(256), 0, (hipStream_t)stream, pf, F / 4, W, bias, ids, k, cap, xs);
+  hipLaunchKernelGGL(k_splin_fwd, dim3(B), dim3(256), 0, (hipStream_t)stream, pf, F / 4, W, bias, ids, k, cap, A, xs);
   return launch_check("k_splin_fwd");
 }
 
-int bk_sparse_linear_dx(const float* g, int B, int F, const float* W, const int16_t* ids, const int32_t* k, int cap,
-                        float* dpf, void* stream) {
-  BK_REQUIRE(g && W && ids && k && dpf && B >= 0 && cap > 0, "bad argument");
+int bk_sparse_linear_dx(const float* g, int B, int F, const float* W, int A, const int16_t* ids, const int32_t* k,
+                        int cap, float* dpf, void* stream) {
+  BK_REQUIRE(g && W && ids && k && dpf && B >= 0 && cap > 0 && A > 0, "bad argument");
   BK_REQUIRE(F > 0 && F % 4 == 0 && F / 4 <= kFcMaxF4, "bk_sparse_linear: F a multiple of 4, <= 1024");
   BK_REQUIRE(((uintptr_t)dpf & 15u) == 0 && ((uintptr_t)W & 15u) == 0, "bk_sparse_linear: 16-byte aligned dpf / W");
   if (B == 0) return BK_OK;
-  hipLaunchKernelGGL(k_splin_dx, dim3(B), dim3(256), 0, (hipStream_t)stream, g, F / 4, W, ids, k, cap, dpf);
+  hipLaunchKernelGGL(k_splin_dx, dim3(B), dim3(256), 0, (hipStream_t)stream, g, F / 4, W, ids, k, cap, A, dpf);
   return launch_check("k_splin_dx");
 }
 
@@ -226,11 +235,11 @@ int bk_sparse_linear_index(const int16_t* ids, const int32_t* k, int cap, int B,
   const int grid = (int)((n + 255) / 256);
   hipStream_t s = (hipStream_t)stream;
   if (start == nullptr) {  // phase 1 (the caller zeroed count): per-id counts
-    hipLaunchKernelGGL(k_splin_count, dim3(grid), dim3(256), 0, s, ids, k, cap, B, count);
+    hipLaunchKernelGGL(k_splin_count, dim3(grid), dim3(256), 0, s, ids, k, cap, B, A, count);
     return launch_check("k_splin_count");
   }
   // phase 2 (start = exclusive scan of count, cursor zeroed): the pairs by id
-  hipLaunchKernelGGL(k_splin_fill, dim3(grid), dim3(256), 0, s, ids, k, cap, B, start, cursor, pairs);
+  hipLaunchKernelGGL(k_splin_fill, dim3(grid), dim3(256), 0, s, ids, k, cap, B, A, start, cursor, pairs);
   return launch_check("k_splin_fill");
 }
 

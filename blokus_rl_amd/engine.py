@@ -79,8 +79,8 @@ _SIGS = {
     "bk_bn_forward_ex": (_i, [_vp, ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp,
                               _i, _vp]),
     "bk_bn_backward_ex": (_i, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
-    "bk_sparse_linear_fwd": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
-    "bk_sparse_linear_dx": (_i, [_vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),
+    "bk_sparse_linear_fwd": (_i, [_vp, _i, _i, _vp, _vp, _i, _vp, _vp, _i, _vp, _vp]),
+    "bk_sparse_linear_dx": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _vp]),
     "bk_sparse_linear_index": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "bk_sparse_linear_dw": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "bk_ppo_gae": (_i, [_i, _i, _vp, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp]),

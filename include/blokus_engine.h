@@ -337,8 +337,9 @@ int bk_bn_backward_ex(const float* dy, const float* x, int64_t M, const float* g
 /* The learner's policy Linear (models/blokus_nnet.py:144-146 policy_out, F = 2N^2 -> A) only where
  * compute_loss reads it (neural_network.py:138-157: the log-softmax over each row's legal ids),
  * replacing the three dense fp32 GEMMs of its forward and backward (trainfc.hip). pf [B][F] f32,
- * W [A][F] f32 (nn.Linear's layout), bias [A], ids [B][cap] int16 (the replay's legal ids), k [B];
- * F % 4 == 0, F <= 1024; sums in a fixed order (deterministic).
+ * W [A][F] f32 (nn.Linear's layout), bias [A], ids [B][cap] int16 (the replay's legal ids, read as
+ * unsigned, distinct within a row), k [B]; F % 4 == 0, F <= 1024; an id outside [0, A) is ignored
+ * (its logit is 0, it enters no gradient); sums in a fixed order (deterministic).
  * bk_sparse_linear_fwd: xs[b][j] = bias[ids[b][j]] + pf[b] . W[ids[b][j]] for j < k[b], 0 beyond.
  * bk_sparse_linear_dx:  dpf[b] = sum_{j<k[b]} g[b][j] W[ids[b][j]]   (g [B][cap]).
  * bk_sparse_linear_index: the (id -> pairs) index for dw, in two calls: start NULL (count [A]
@@ -346,10 +347,10 @@ int bk_bn_backward_ex(const float* dy, const float* x, int64_t M, const float* g
  *   cursor [A] zeroed: pairs [B cap] = the pair indices b cap + j grouped by id.
  * bk_sparse_linear_dw:  dW[a] = sum over the rows b holding id a of g[b][j] pf[b] (ascending b),
  *   db[a] likewise; every row written (zero where no row holds a); B <= 4096. */
-int bk_sparse_linear_fwd(const float* pf, int B, int F, const float* W, const float* bias, const int16_t* ids,
+int bk_sparse_linear_fwd(const float* pf, int B, int F, const float* W, const float* bias, int A, const int16_t* ids,
                          const int32_t* k, int cap, float* xs, void* stream);
-int bk_sparse_linear_dx(const float* g, int B, int F, const float* W, const int16_t* ids, const int32_t* k, int cap,
-                        float* dpf, void* stream);
+int bk_sparse_linear_dx(const float* g, int B, int F, const float* W, int A, const int16_t* ids, const int32_t* k,
+                        int cap, float* dpf, void* stream);
 int bk_sparse_linear_index(const int16_t* ids, const int32_t* k, int cap, int B, int A, int32_t* count,
                            int32_t* start, int32_t* cursor, int32_t* pairs, void* stream);
 int bk_sparse_linear_dw(const float* g, const float* pf, int B, int F, int cap, int A, const int32_t* start,

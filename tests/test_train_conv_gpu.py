@@ -373,6 +373,31 @@ def test_sparse_policy_linear_matches_dense():
     held[ids[valid].long()] = True
     assert bool((dW[~held] == 0).all()) and bool((db[~held] == 0).all()) and int((~held).sum()) > 0
 
+    # ids outside [0, A) inside k (-1 = 65535 unsigned, A itself): logit 0, no gradient, no access
+    # past W; the rest of the row unchanged
+    bad = ids.clone()
+    rows = [b for b in range(2, B) if int(k[b]) >= 2][:20]
+    for i, b in enumerate(rows):
+        bad[b, i % 2] = -1 if i % 3 else A
+    pd, Wd, bd = (t.float().cuda().requires_grad_() for t in (pf, W, bias))
+    xb = SparsePolicyLinear.apply(pd, Wd, bd, bad.cuda(), k.to(torch.int32).cuda())
+    gb = gy.clone()
+    for i, b in enumerate(rows):
+        gb[b, i % 2] = 0.0  # the reference: those pairs absent
+    xb.backward(gb.float().cuda())
+    xb = xb.detach().cpu().double()
+    for i, b in enumerate(rows):
+        assert float(xb[b, i % 2]) == 0.0
+    keep = valid.clone()
+    for i, b in enumerate(rows):
+        keep[b, i % 2] = False
+    assert float(((xb - gat.detach()) * keep).abs().max()) <= 1e-5 * float(gat.detach().abs().max())
+    pr2, Wr2, br2 = (t.clone().requires_grad_() for t in (pf, W, bias))
+    gat2 = torch.gather(torch.nn.functional.linear(pr2, Wr2, br2), 1, ids.long().clamp(min=0)) * keep
+    gat2.backward(gb * keep)
+    for a, r in ((pd.grad.cpu().double(), pr2.grad), (Wd.grad.cpu().double(), Wr2.grad), (bd.grad.cpu().double(), br2.grad)):
+        assert float((a - r).abs().max()) <= 1e-5 * float(r.abs().max()), float((a - r).abs().max())
+
 
 def test_learner_sparse_head_matches_dense_head():
     """The learner's step with the sparse policy head (Learner.sparse_head: logits at the legal ids
