@@ -295,7 +295,7 @@ def test_fused_conv_bn_relu_matches_fp64():
         for a, r in ((xd.grad, xr.grad), (wd.grad, wr.grad), (gd.grad, gr.grad), (btd.grad, btr.grad)):
             assert float((a.double().cpu() - r).abs().max()) <= 2e-5 * scale(r), (relu, scale(r))
         assert float(bd.grad.abs().max()) <= 1e-6 * float(gy.abs().sum(dim=(0, 2, 3)).max())
-        assert float((rm.double().cpu() - 0.1 * z.detach().mean(dim=(0, 2, 3))).abs().max()) <= 1e-6 * float(z.abs().max())
+        assert float((rm.double().cpu() - 0.1 * z.detach().mean(dim=(0, 2, 3))).abs().max()) <= 1e-6 * float(z.detach().abs().max())
 
 
 def test_train_resnet_matches_unfused_device_path():
