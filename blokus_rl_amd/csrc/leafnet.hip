@@ -27,6 +27,10 @@
 #include "../../include/blokus_engine.h"
 #include "ctx.h"
 
+// the MFMA accumulators in VGPRs: the epilogue's VALU reads them without 100 v_accvgpr_read per
+// layer (AGPRs: 159.7 vs 157.9 us a launch, self-play +0.9%, three interleaved rounds on one box;
+// x0 still waits in AGPRs)
+#define BK_LN_VACC 1
 #include "leafnet_common.h"
 
 namespace bk {

@@ -47,7 +47,7 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 // The slot of group g is g % kLnSlots in every chunk, which needs NG % kLnSlots == 0: the board's
 // groups are padded with spare ones (all columns spare: halo reads, no writes) up to a multiple.
 #ifndef BK_LN_VACC
-#define BK_LN_VACC 0  // the MFMA accumulators in VGPRs (1: leafnet_w3.hip, whose AGPRs hold U) or AGPRs (0)
+#define BK_LN_VACC 0  // the MFMA accumulators in VGPRs (1: leafnet.hip, and leafnet_w3.hip, whose AGPRs hold U) or AGPRs (0)
 #endif
 #if BK_LN_VACC
 #define BK_ACC_W "=&v"
@@ -229,8 +229,8 @@ __device__ __forceinline__ void ln_prime(h16x8 (&rb)[kLnSlots][2], const unsigne
 // One K chunk over the board's NG pixel groups: acc[g] += ah*bh + al*bh + ah*bl with the group's
 // B fragments from the ring, whose reads run kLnPf groups ahead and on into the next chunk
 // (coff_next; on the last chunk of a layer any in-grid offset: those reads are never consumed).
-// The MFMAs are inline asm with the accumulator in place in AGPRs (srcC = vdst: back-to-back
-// accumulation, no copies); INIT starts the accumulators from 0.
+// The MFMAs are inline asm with the accumulator in place (srcC = vdst: back-to-back accumulation,
+// no copies; VGPRs or AGPRs per BK_LN_VACC); INIT starts the accumulators from 0.
 template <int NG, bool INIT, int HALF>
 __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, const unsigned char* grid,
                                          const int (&pb)[NG], int coff, int coff_next, h16x8 (&rb)[kLnSlots][2]) {
