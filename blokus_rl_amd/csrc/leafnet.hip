@@ -33,8 +33,14 @@
 #define BK_LN_VACC 1
 #include "leafnet_common.h"
 
+#ifndef BK_LN_EPIW
+#define BK_LN_EPIW 1  // a tower conv's outputs stored group by group inside its epilogue (0: all after it)
+#endif
+
 namespace bk {
 namespace {
+
+constexpr bool kLnEpiWrite = BK_LN_EPIW != 0;
 
 template <int N>
 __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __restrict__ obs,
@@ -181,7 +187,13 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
   // reduction is needed before the split), split, and the packed halves kept in acc's registers
   // until every wave has finished reading the grid (bar 1), then written; the lane's max |y|
   // (unscaled) is returned for the next layer's bound. !OUT (the last conv): y stays in acc.
-  auto epilogue = [&](f32x4 sv, f32x4 bv, bool relu, bool residual, const f32x4 (&x0)[NG], bool out, int ex_out) {
+  // WRITE (with OUT, after a barrier that every wave has finished reading the grid): each group's
+  // halves are stored into the grid as soon as they are split, so the LDS stores drain under the
+  // next groups' VALU instead of after all of it.
+  auto epilogue = [&](f32x4 sv, f32x4 bv, bool relu, bool residual, const f32x4 (&x0)[NG], bool out, int ex_out,
+                      bool write = false) {
+    const int o = 2 * wave + (ks >> 1);
+    unsigned char* wbase = act + ((o & 3) * 4 + (o >> 2) * 2) * PL + (ks & 1) * 8;  // as write_act
     // OUT folds the output scale 2^ex_out into s and bias (exact: powers of two), so y comes out
     // scaled and goes straight to the split; the lane maximum is unscaled once at the end
     const int k = out ? ex_out : 0;
@@ -204,8 +216,15 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         unsigned h0, h1, l0, l1;
         split2(y01.x, y01.y, h0, l0);
         split2(y23.x, y23.y, h1, l1);
-        acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
-                       __builtin_bit_cast(float, l1)};
+        if (write) {
+          if (is_valid(g)) {
+            *reinterpret_cast<u32x2*>(wbase + slot_b(g)) = u32x2{h0, h1};
+            *reinterpret_cast<u32x2*>(wbase + slot_b(g) + PL) = u32x2{l0, l1};
+          }
+        } else {
+          acc[g] = f32x4{__builtin_bit_cast(float, h0), __builtin_bit_cast(float, h1), __builtin_bit_cast(float, l0),
+                         __builtin_bit_cast(float, l1)};
+        }
       } else {
         acc[g] = f32x4{y01.x, y01.y, y23.x, y23.y};
       }
@@ -330,6 +349,19 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         max_in = fmaxf(max_in, mx);  // keep the arithmetic live
         ex = ex_out;
       }
+    } else if (!last && kLnEpiWrite) {
+      const int ex_out = scale_exp(bnd_a * max_in + bnd_b);  // = out_exp(layer + 1, max_in)
+      if (layer == 1) LNSTAMP(21, __builtin_amdgcn_s_memtime());
+      __syncthreads();  // every wave has finished reading the grid: the outputs go in place as made
+      if (layer == 1) LNSTAMP(22, __builtin_amdgcn_s_memtime());
+      const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out, true);
+      if (layer == 1) LNSTAMP(23, __builtin_amdgcn_s_memtime());
+      post_max(mx, (layer + 1) & 1);
+      if (layer == 1) LNSTAMP(24, __builtin_amdgcn_s_memtime());
+      __syncthreads();
+      if (layer == 1) LNSTAMP(25, __builtin_amdgcn_s_memtime());
+      max_in = board_max((layer + 1) & 1);
+      ex = ex_out;
     } else if (!last) {
       const int ex_out = scale_exp(bnd_a * max_in + bnd_b);  // = out_exp(layer + 1, max_in)
       const float mx = epilogue(sv, bv, !(layer & 1), false, x0, true, ex_out);
