@@ -41,6 +41,10 @@ namespace bk {
 namespace {
 
 constexpr bool kLnEpiWrite = BK_LN_EPIW != 0;
+#ifndef BK_LN_IL
+#define BK_LN_IL 1  // the tower's B-fragment reads between the MFMAs of each triple (ln_chunk_il)
+#endif
+constexpr bool kLnInterleave = BK_LN_IL != 0;
 
 template <int N>
 __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __restrict__ obs,
@@ -330,11 +334,20 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_leafnet_x3(const float* __res
         wq[sn][1] = wload(nl, cn - 18, 1);
       }
       const h16x8* w = wq[c % (kLnWpf + 1)];
-      if (c == 0)
-        ln_chunk<NG, true, PL>(acc, w[0], w[1], act, ab, coff_of(0), coff_of(1), rb);
-      else
-        ln_chunk<NG, false, PL>(acc, w[0], w[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+      if constexpr (kLnInterleave) {
+        if (c == 0)
+          ln_chunk_il<NG, true, PL>(acc, w[0], w[1], act, ab, coff_of(0), coff_of(1), rb);
+        else
+          ln_chunk_il<NG, false, PL>(acc, w[0], w[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+      } else {
+        if (c == 0)
+          ln_chunk<NG, true, PL>(acc, w[0], w[1], act, ab, coff_of(0), coff_of(1), rb);
+        else
+          ln_chunk<NG, false, PL>(acc, w[0], w[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+      }
     }
+    // the last chunk's read-ahead (ln_chunk_il: untracked) lands before its registers are reused
+    if constexpr (kLnInterleave) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ln_mfma_drain(acc);
     if (layer < 8) LNSTAMP(4 + 2 * layer, __builtin_amdgcn_s_memtime());
     const bool last = layer + 1 == nlayers;

@@ -273,6 +273,73 @@ __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, c
   }
 }
 
+// ln_chunk with each group's two B-fragment reads (kLnPf groups ahead) issued between its three
+// MFMAs in one asm block: wait (lgkmcnt(2): the reads of the two blocks before are the only ones
+// still allowed in flight), MFMA, read hi, MFMA, read lo, MFMA — one instruction in each MFMA's
+// issue gap instead of two reads and a wait in one (a 16x16x32 MFMA holds the SIMD's issue for 8
+// of its 16 cycles: MI355X_MICROARCH.md). The reads are invisible to the compiler: the grid offsets
+// must be compile-time constants (immediates), the ring registers are only read by later blocks
+// (after their wait), and the caller waits lgkmcnt(0) after its last chunk, before the ring
+// registers can be reused. Same MFMAs on the same operands as ln_chunk: the sums are bitwise equal.
+template <int NG, bool INIT, int HALF>
+__device__ __forceinline__ void ln_chunk_il(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, const unsigned char* grid,
+                                            const int (&pb)[NG], int coff, int coff_next, h16x8 (&rb)[kLnSlots][2]) {
+  static_assert(NG % kLnSlots == 0, "ln_chunk_il: the ring slot of a group must not depend on the chunk");
+  const unsigned gbase = (unsigned)(uintptr_t)grid;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int gp = g + kLnPf;
+    const unsigned addr = gbase + (unsigned)(gp < NG ? pb[gp] : pb[gp - NG]);
+    h16x8& n0 = rb[gp % kLnSlots][0];
+    h16x8& n1 = rb[gp % kLnSlots][1];
+    if (gp < NG) {
+      if (INIT)
+        asm volatile(
+            "s_waitcnt lgkmcnt(2)\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %5, 0\n\t"
+            "ds_read_b128 %1, %7 offset:%8\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
+            "ds_read_b128 %2, %7 offset:%9\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
+            : BK_ACC_W(acc[g]), "=&v"(n0), "=&v"(n1)
+            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff), "i"(coff + HALF));
+      else
+        asm volatile(
+            "s_waitcnt lgkmcnt(2)\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %5, %0\n\t"
+            "ds_read_b128 %1, %7 offset:%8\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
+            "ds_read_b128 %2, %7 offset:%9\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
+            : BK_ACC_RW(acc[g]), "=&v"(n0), "=&v"(n1)
+            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff), "i"(coff + HALF));
+    } else {
+      if (INIT)
+        asm volatile(
+            "s_waitcnt lgkmcnt(2)\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %5, 0\n\t"
+            "ds_read_b128 %1, %7 offset:%8\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
+            "ds_read_b128 %2, %7 offset:%9\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
+            : BK_ACC_W(acc[g]), "=&v"(n0), "=&v"(n1)
+            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff_next),
+              "i"(coff_next + HALF));
+      else
+        asm volatile(
+            "s_waitcnt lgkmcnt(2)\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %5, %0\n\t"
+            "ds_read_b128 %1, %7 offset:%8\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
+            "ds_read_b128 %2, %7 offset:%9\n\t"
+            "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
+            : BK_ACC_RW(acc[g]), "=&v"(n0), "=&v"(n1)
+            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff_next),
+              "i"(coff_next + HALF));
+    }
+  }
+}
+
 // the accumulators are written by MFMAs the compiler cannot see: wait out the MFMA write ->
 // VALU read latency before the epilogue reads them. Each accumulator then passes through an empty
 // asm that follows the wait (volatile asm keeps its order), so no read of it can be scheduled
