@@ -56,7 +56,7 @@ __host__ __device__ constexpr int ln_chunks(int cin) { return cin == 64 ? 18 : 3
 #define BK_ACC_W "=&a"
 #define BK_ACC_RW "+a"
 #endif
-// read-ahead: 2 groups of B fragments (4: no gain), 1 chunk of weights (2: no gain)
+// read-ahead: 2 groups of B fragments (3, 4: no gain, also with ln_chunk_il), 1 chunk of weights (2: no gain)
 constexpr int kLnPf = 2, kLnSlots = 5, kLnWpf = 1;
 static_assert(kLnPf >= 1 && kLnPf < kLnSlots, "kLnPf");
 __host__ __device__ constexpr int ln_groups(int N) { return ((N * N + 15) / 16 + kLnSlots - 1) / kLnSlots * kLnSlots; }
@@ -274,8 +274,8 @@ __device__ __forceinline__ void ln_chunk(f32x4 (&acc)[NG], h16x8 ah, h16x8 al, c
 }
 
 // ln_chunk with each group's two B-fragment reads (kLnPf groups ahead) issued between its three
-// MFMAs in one asm block: wait (lgkmcnt(2): the reads of the two blocks before are the only ones
-// still allowed in flight), MFMA, read hi, MFMA, read lo, MFMA — one instruction in each MFMA's
+// MFMAs in one asm block: wait (lgkmcnt(2 (kLnPf - 1)): the reads of the kLnPf - 1 blocks before
+// are the only ones still allowed in flight), MFMA, read hi, MFMA, read lo, MFMA — one instruction in each MFMA's
 // issue gap instead of two reads and a wait in one (a 16x16x32 MFMA holds the SIMD's issue for 8
 // of its 16 cycles: MI355X_MICROARCH.md). The reads are invisible to the compiler: the grid offsets
 // must be compile-time constants (immediates), the ring registers are only read by later blocks
@@ -295,28 +295,28 @@ __device__ __forceinline__ void ln_chunk_il(f32x4 (&acc)[NG], h16x8 ah, h16x8 al
     if (gp < NG) {
       if (INIT)
         asm volatile(
-            "s_waitcnt lgkmcnt(2)\n\t"
+            "s_waitcnt lgkmcnt(%10)\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %3, %5, 0\n\t"
             "ds_read_b128 %1, %7 offset:%8\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
             "ds_read_b128 %2, %7 offset:%9\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
             : BK_ACC_W(acc[g]), "=&v"(n0), "=&v"(n1)
-            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff), "i"(coff + HALF));
+            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff), "i"(coff + HALF), "i"(2 * (kLnPf - 1)));
       else
         asm volatile(
-            "s_waitcnt lgkmcnt(2)\n\t"
+            "s_waitcnt lgkmcnt(%10)\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %3, %5, %0\n\t"
             "ds_read_b128 %1, %7 offset:%8\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
             "ds_read_b128 %2, %7 offset:%9\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
             : BK_ACC_RW(acc[g]), "=&v"(n0), "=&v"(n1)
-            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff), "i"(coff + HALF));
+            : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff), "i"(coff + HALF), "i"(2 * (kLnPf - 1)));
     } else {
       if (INIT)
         asm volatile(
-            "s_waitcnt lgkmcnt(2)\n\t"
+            "s_waitcnt lgkmcnt(%10)\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %3, %5, 0\n\t"
             "ds_read_b128 %1, %7 offset:%8\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
@@ -324,10 +324,10 @@ __device__ __forceinline__ void ln_chunk_il(f32x4 (&acc)[NG], h16x8 ah, h16x8 al
             "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
             : BK_ACC_W(acc[g]), "=&v"(n0), "=&v"(n1)
             : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff_next),
-              "i"(coff_next + HALF));
+              "i"(coff_next + HALF), "i"(2 * (kLnPf - 1)));
       else
         asm volatile(
-            "s_waitcnt lgkmcnt(2)\n\t"
+            "s_waitcnt lgkmcnt(%10)\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %3, %5, %0\n\t"
             "ds_read_b128 %1, %7 offset:%8\n\t"
             "v_mfma_f32_16x16x32_f16 %0, %4, %5, %0\n\t"
@@ -335,7 +335,7 @@ __device__ __forceinline__ void ln_chunk_il(f32x4 (&acc)[NG], h16x8 ah, h16x8 al
             "v_mfma_f32_16x16x32_f16 %0, %3, %6, %0"
             : BK_ACC_RW(acc[g]), "=&v"(n0), "=&v"(n1)
             : "v"(ah), "v"(al), "v"(rb[g % kLnSlots][0]), "v"(rb[g % kLnSlots][1]), "v"(addr), "i"(coff_next),
-              "i"(coff_next + HALF));
+              "i"(coff_next + HALF), "i"(2 * (kLnPf - 1)));
     }
   }
 }
