@@ -17,6 +17,10 @@
 
 #include "leafnet_common.h"
 
+#ifndef BK_CONV_IL
+#define BK_CONV_IL 1  // k_conv_x3: ln_chunk_il (the B-fragment reads between the MFMAs)
+#endif
+
 namespace bk {
 namespace {
 
@@ -126,11 +130,22 @@ __global__ __launch_bounds__(kLnThreads, 1) void k_conv_x3(const float* __restri
         wq[sn][1] = wload(cn, 1);
       }
       const h16x8* wc = wq[c % (kLnWpf + 1)];
+#if BK_CONV_IL
+      // the B-fragment reads between each triple's MFMAs (leafnet_common.h ln_chunk_il)
+      if (c == 0)
+        ln_chunk_il<NG, true, PL>(acc, wc[0], wc[1], act, ab, coff_of(0), coff_of(1), rb);
+      else
+        ln_chunk_il<NG, false, PL>(acc, wc[0], wc[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+#else
       if (c == 0)
         ln_chunk<NG, true, PL>(acc, wc[0], wc[1], act, ab, coff_of(0), coff_of(1), rb);
       else
         ln_chunk<NG, false, PL>(acc, wc[0], wc[1], act, ab, coff_of(c), coff_of(c + 1 < 18 ? c + 1 : c), rb);
+#endif
     }
+#if BK_CONV_IL
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last chunk's untracked read-ahead
+#endif
     ln_mfma_drain(acc);
 
     // y = acc * inv * 2^-ex + bias, NHWC
