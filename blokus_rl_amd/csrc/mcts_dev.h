@@ -146,7 +146,10 @@ __device__ __forceinline__ void wave_argmax(double& best, int& bi) {
 // memory round trip: each lane loads all its children's (P, N, Q, id) first, the visit sum is
 // the wave's integer sum of N, then the lane scans its children in index order.
 constexpr int kSelB = 12;
-constexpr int kMaskWpb = 16;  // waves that take orientations in a leaf bitmask (the rest idle)
+// waves that take orientations in a leaf bitmask (the rest idle): 8 slices (every 8th
+// orientation) — each claiming wave pays its own row context, so 16 slices cost more setup than
+// they save (self-play +0.3% at plies 2-8 and 8-18 vs 16; 4: in between; round 6, lib_ab.sh)
+constexpr int kMaskWpb = 8;
 // eps: the term under the square root (mcts.py:43: 1e-6 with epsilon_fix, the default, else 0)
 __device__ __forceinline__ int select_child(const DevMcts& m, int64_t off, int K, double cp, int& id_out,
                                             double eps = 1e-6) {
