@@ -321,7 +321,7 @@ def test_train_resnet_matches_unfused_device_path():
         p, v = model(batch["observation"].contiguous(memory_format=torch.channels_last))
         loss = alphazero_loss(p, v, batch)
         loss.backward()
-        out[fused] = (float(loss), {k: t.grad.detach().clone() for k, t in model.named_parameters()})
+        out[fused] = (float(loss.detach()), {k: t.grad.detach().clone() for k, t in model.named_parameters()})
     assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0])
     for k, g0 in out[False][1].items():
         if k in ("conv1.bias", "policy_conv.bias", "value_conv.bias") or (
