@@ -424,7 +424,7 @@ def test_learner_sparse_head_matches_dense_head():
             p, v = model(obs)
             loss = alphazero_loss(p, v, batch)
         loss.backward()
-        out[sparse] = (float(loss), {n: t.grad.detach().clone() for n, t in model.named_parameters()})
+        out[sparse] = (float(loss.detach()), {n: t.grad.detach().clone() for n, t in model.named_parameters()})
     assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0])
     for n, g0 in out[False][1].items():
         if n in ("conv1.bias", "policy_conv.bias", "value_conv.bias") or (
