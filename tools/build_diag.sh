@@ -7,8 +7,8 @@ cd blokus_rl_amd/csrc
 mkdir -p ../_lib/diag/o
 rm -f ../_lib/diag/o/*.o
 pids=()
-for f in env.hip mcts.hip vecenv.hip train.hip ppo.hip netops.hip conv.hip leafnet.hip; do
-  XF=""; [ "$f" = conv.hip ] && XF="-fno-slp-vectorize"
+for f in env.hip mcts.hip vecenv.hip train.hip trainconv.hip trainbn.hip trainfc.hip ppo.hip netops.hip conv.hip leafnet.hip leafnet_w3.hip ply.hip; do
+  XF=""; [ "$f" = conv.hip ] && XF="-fno-slp-vectorize"; [ "$f" = leafnet_w3.hip ] && XF="-mllvm -pragma-unroll-threshold=1000000"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function -DBK_STAMPS $XF \
     -c -o ../_lib/diag/o/$f.o $f &
   pids+=($!)
